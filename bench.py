@@ -1,0 +1,240 @@
+"""Benchmark: Mpixels/s of the render path (BASELINE.json metric) on 1..N MI355X.
+
+    python bench.py --gpus N --steps K --warmup W [--config C2] [--mode frames|tiles]
+
+A *step* is one frame of the configuration through the public API — ``HipRenderer.raytrace_scene(
+camera.position, get_ray_directions(camera), scene)``: scene packing (cached by content), primary
+ray generation, nearest hit, shadow rays, shading and every reflection level up to the cap, with the
+unclipped colour left in HBM (float32 [3, W*H]). PNG encoding is not part of a step.
+
+Default workload (N=1): BASELINE.json configs[1] — the README scene at 1920x1080, 3 reflection
+bounces. ``--mode frames`` (default, weak scaling): every rank renders its own frames, no collective
+in the loop (the frame sharding of config C5). ``--mode tiles`` (strong scaling): every rank renders
+its interleaved row tile of ONE frame and the tiles are gathered to rank 0 (RCCL) every step.
+
+Timing: W untimed warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
+The dominant kernel's own time is measured live with HIP events recorded by the library on the
+launch stream (rtx_profile_*), for the roofline. Rank 0 also times the CPU oracle (NumPy float64,
+single core) on a bounded sample of the same workload.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+# MI355X peaks (MI355X_MICROARCH.md; FP64 vector = half the FP32 vector rate, datasheet 78.6 TF)
+PEAK_FP64_TFLOPS = 78.6
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="C2", help="C1|C2|C2main|C3|C4|C5 (python_ray_tracer_amd/scenes.py)")
+    ap.add_argument("--mode", default="frames", choices=["frames", "tiles"])
+    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--out", default="f32", choices=["f32", "f64", "u8"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0: skip)")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    spec, B = scenes.CONFIGS[args.config]()
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    scene = scenes.build_scene(spec)
+    dtype = torch.float64 if args.out == "f64" else torch.float32
+    r = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev)
+
+    if args.mode == "frames":
+        def step():
+            if args.out == "u8":
+                return r.render_tile(scene, out="u8")
+            return r.raytrace_scene(scene.camera.position, r.get_ray_directions(scene.camera), scene)
+        px_per_step = W * H * world
+    else:
+        from python_ray_tracer_amd.application import render_frame_distributed
+
+        def step():
+            if world == 1:
+                return r.render_tile(scene, out="u8" if args.out == "u8" else None)
+            return render_frame_distributed(scene, r, row_block=args.row_block,
+                                            gather="u8" if args.out == "u8" else "color")
+        px_per_step = W * H
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    L.profile_enable(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms, kern_n = L.profile_collect()
+    L.profile_enable(0)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # algorithmic work of one launch, from the kernel's own counters (checked against the oracle in
+    # tests/test_gpu_parity.py): 15 flops / primary ray, 20 / ray-sphere test, 200 / shaded hit
+    rs = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev, collect_stats=True)
+    if args.mode == "frames" or world == 1:
+        rs.render_tile(scene)
+        n_px_launch = W * H
+    else:
+        from python_ray_tracer_amd.tiling import n_local_rows
+
+        rs.render_tile(scene, args.row_block, world, rank)
+        n_px_launch = W * n_local_rows(H, args.row_block, world, rank)
+    st = rs.stats()
+    S = len(spec["spheres"])
+    R_tr, R_sh = sum(st["rays"]), sum(st["hits"])
+    flops = 15 * n_px_launch + 20 * S * (R_tr + R_sh) + 200 * R_sh
+    out_bytes = {"f32": 12, "f64": 24, "u8": 3}[args.out]
+    alg_bytes = out_bytes * n_px_launch + 8 * len(r.scene_blob(scene)[0])  # framebuffer write + scene read
+    kern_avg_s = kern_ms / 1e3 / max(kern_n, 1)
+    achieved_tflops = flops / kern_avg_s / 1e12
+    achieved_gbs = alg_bytes / kern_avg_s / 1e9
+
+    traffic = None
+    pmc = REPO / "profiles" / "pmc_traffic.json"
+    if pmc.exists():
+        try:
+            d = json.loads(pmc.read_text())
+            traffic = d.get(args.config, {}).get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(spec, B, args.cpu_seconds)
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = px_per_step * args.steps / elapsed / 1e6
+        line = {
+            "metric": "Mpixels/sec @1920x1080, 3 reflection bounces" if args.config in ("C2", "C2main")
+            else f"Mpixels/sec ({args.config})",
+            "value": round(value, 3),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "frames" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config}: " + {
+                "C1": "README scene 960x540",
+                "C2": "README scene (BASELINE configs[1]) 1920x1080",
+                "C2main": "main.py scene 1920x1080",
+                "C3": "16 random spheres + checker ground 3840x2160 seed 0",
+                "C4": "64 random spheres + checker ground 7680x4320 seed 0",
+                "C5": "16 random spheres 1920x1080 seed 0"}[args.config] + f", {B} bounces",
+                "width": W, "height": H, "max_bounces": B, "spheres": S, "output": args.out,
+                "mode": args.mode, "parallelism": f"{args.mode}x{world}"},
+            "roofline": {
+                "bound": "valu",
+                "kernel": f"k_render_fast<{B}>",
+                "achieved": round(achieved_tflops, 4),
+                "peak": PEAK_FP64_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / PEAK_FP64_TFLOPS, 5),
+                "traffic": traffic,
+                "kernel_ms": round(kern_avg_s * 1e3, 5),
+                "flops_per_launch": flops,
+                "rays_per_level": st["rays"],
+                "hits_per_level": st["hits"],
+                "hbm": {"achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "alg_bytes_per_launch": alg_bytes},
+                "note": "FP64 VALU-bound megakernel (no dense contraction, no MFMA); achieved = algorithmic "
+                        "FLOPs (SURVEY.md 8d model, kernel counters) / kernel time (HIP events, launch stream)",
+            },
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["gpu_vs_cpu"] = round(value / cpu["value"], 1)
+        s = json.dumps(line)
+        print(s)
+        if args.json_out:
+            Path(args.json_out).write_text(s + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(spec, B, budget_s):
+    """The CPU oracle (NumPy float64, the reference's algorithm; single process => 1 core) on full
+    frames of the same configuration until ``budget_s`` seconds of CPU work (at least one frame);
+    ray generation + trace, no PNG — the same region as a GPU step."""
+    import platform
+
+    from oracle import numpy_oracle as O
+
+    sc = O.scene_from_spec(spec)
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        O.render(sc, B)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start >= budget_s or len(times) >= 50:
+            break
+    best = min(times)
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(W * H / best / 1e6, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": f"{len(times)} full {W}x{H} frames, B={B}, best of {len(times)} "
+                      f"(median {sorted(times)[len(times) // 2]:.3f}s); oracle/numpy_oracle.py, "
+                      f"{cpu_model or platform.processor()}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,202 @@
+/*
+ * rtx_hip.h — C ABI of the MI355X (gfx950) render-path library  librtx_hip.so
+ *
+ * This is the drop-in boundary for the reference's NumPy render backend
+ * (/root/reference/ray_tracer/infrastructure/numpy/). Every entry point below replaces one
+ * reference interface; the Python host layer (python_ray_tracer_amd/infrastructure/hip/) calls
+ * them through ctypes with device pointers owned by torch tensors. Signatures are plain C:
+ * pointers, sizes and an opaque stream handle (a hipStream_t) — no torch types.
+ *
+ *   rtx_render_camera   <- NumpyRenderer.get_ray_directions + NumpyRenderer.raytrace_scene at
+ *                          level 0 with the camera origin   (base.py:123-141, base.py:91-121,
+ *                          and the recursion through shader.py:63-161), fused; also one row tile
+ *                          of the frame for the multi-GPU path (application.py:43-52 gains it)
+ *   rtx_trace_rays      <- NumpyRenderer.raytrace_scene(ray_origin, dirs, scene) for an arbitrary
+ *                          batch of rays                      (base.py:91-121)
+ *   rtx_ray_directions  <- NumpyRenderer.get_ray_directions  (base.py:123-141)
+ *   rtx_sphere_intersect<- NumpySphere.intersect             (shape.py:28-51)
+ *   rtx_quantize_u8     <- NumpyRenderer.save_image's (255*clip(c,0,1)).astype(uint8)
+ *                                                             (base.py:143-151)
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers (hipMalloc / torch caching allocator), read-only
+ *    unless documented as output. Vectors are structure-of-arrays [3][n] float64, exactly the
+ *    x/y/z arrays of the reference's NumpyVector3D. A shared origin (the reference passes the
+ *    camera position as Python scalars at level 0) is origin_stride == 0 and 3 doubles.
+ *  - Work is enqueued asynchronously on `stream` (hipStream_t; NULL = the null stream); the caller
+ *    synchronises. Entry points never allocate, never synchronise, and are graph-capturable.
+ *  - Return 0 on success, a negative RTX_E_* code otherwise; rtx_last_error() gives a message
+ *    (thread-local). The Python layer raises RuntimeError on non-zero, like TORCH_CHECK would.
+ *  - Scene blob: float64 array built by the host packer (scene_pack.py), layout below. It holds
+ *    everything the reference reads from Scene3D during a render.
+ *  - Arithmetic is IEEE float64 with no contraction (built with -ffp-contract=off), in the
+ *    reference's operation order; sin and pow are the only non-correctly-rounded operations
+ *    (≈1 ulp, as NumPy's SIMD versions are).
+ */
+#ifndef RTX_HIP_H
+#define RTX_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTX_ABI_VERSION 1
+
+/* ---- scene blob layout (float64 words) ---- */
+enum {
+  RTX_HDR_WORDS = 64,  /* header */
+  RTX_GEOM_WORDS = 8,  /* per sphere, at RTX_HDR_WORDS + s*RTX_GEOM_WORDS            */
+  RTX_MAT_WORDS = 24,  /* per sphere, at RTX_HDR_WORDS + S*RTX_GEOM_WORDS + s*MAT    */
+  RTX_MAX_DOMES = 8,
+  RTX_MAX_SPHERES = 1024
+};
+
+/* header words */
+enum {
+  RTX_H_MAGIC = 0,   /* RTX_MAGIC */
+  RTX_H_NSPH = 1,    /* S */
+  RTX_H_CAM = 2,     /* camera position x,y,z (also V target on every level, shader.py:76) */
+  RTX_H_LIGHT = 5,   /* scene.lights[0].position (shader.py:75) */
+  RTX_H_DOMEC = 8,   /* colour of the LAST DomeLight, white if none (shader.py:237-241) */
+  RTX_H_NDOME = 11,  /* number of DomeLights */
+  RTX_H_DOMEI = 12,  /* their intensities, scene order (RTX_MAX_DOMES words) */
+  RTX_H_XSTART = 20, /* np.linspace(-1, 1, W): start, step, stop, (W > 1) endpoint fix */
+  RTX_H_XSTEP = 21,
+  RTX_H_XSTOP = 22,
+  RTX_H_XFIX = 23,
+  RTX_H_YSTART = 24, /* np.linspace(1/ar + .25, -1/ar + .25, H) */
+  RTX_H_YSTEP = 25,
+  RTX_H_YSTOP = 26,
+  RTX_H_YFIX = 27,
+  RTX_H_VZ = 28,     /* 0 - camera.z (base.py:141) */
+  RTX_H_VZ2 = 29,    /* VZ*VZ */
+  RTX_H_W = 30,
+  RTX_H_H = 31,
+  RTX_H_CAMOO = 32   /* |camera|^2 = camera.dot(camera) (shape.py:35 with the level-0 origin) */
+};
+#define RTX_MAGIC 5527384.0 /* 'RTX1' */
+
+/* per-sphere geometry words */
+enum {
+  RTX_G_CX = 0, RTX_G_CY = 1, RTX_G_CZ = 2,
+  RTX_G_CC = 3,    /* abs(position) = C.C                 (shape.py:35)  */
+  RTX_G_RR = 4,    /* radius*radius                       (shape.py:36)  */
+  RTX_G_INVR = 5,  /* 1.0/radius                          (shader.py:74) */
+  RTX_G_C0 = 6     /* c for the camera origin: ((C.C + O.O) - 2*C.O) - r*r, O = camera */
+};
+
+/* per-sphere material words (NumpyShader, shader.py:36-54; derived constants computed on the
+ * host in Python with the reference's own expressions) */
+enum {
+  RTX_M_G = 0,       /* specular_gain                                      */
+  RTX_M_DG = 1,      /* diffuse_gain                                       */
+  RTX_M_TEX = 2,     /* 0 = Texture (constant colour), 1 = TextureChecker  */
+  RTX_M_TR = 3, RTX_M_TG = 4, RTX_M_TB = 5, /* Texture colour            */
+  RTX_M_A2 = 6,      /* alpha**2, alpha = specular_roughness**2 (:294-296) */
+  RTX_M_A2M1 = 7,    /* alpha**2 - 1                                       */
+  RTX_M_1MA2 = 8,    /* 1 - alpha**2                                       */
+  RTX_M_F0 = 9,      /* ((ior-1)/(ior+1))**2                     (:290)    */
+  RTX_M_1MF0 = 10,   /* 1 - F0                                             */
+  RTX_M_IG = 11,     /* iridescence_gain                                   */
+  RTX_M_TFW = 12,    /* thin_film_weight                                   */
+  RTX_M_TFT = 13,    /* thin_film_thickness                                */
+  RTX_M_HS = 14,     /* (thin_film_ior - 1.0)/2.0                (:215)    */
+  RTX_M_1MHS = 15,   /* 1.0 - hue_shift                                    */
+  RTX_M_ROUGH = 16,  /* specular_roughness (informational)                 */
+  RTX_M_REFL = 17,   /* reflection_gain (stored, never read: shader.py:45) */
+  RTX_M_IOR = 18,
+  RTX_M_TFIOR = 19
+};
+
+/* output kinds */
+enum {
+  RTX_OUT_F32_SOA = 0, /* float  [3][n]  unclipped colour                     */
+  RTX_OUT_F64_SOA = 1, /* double [3][n]  unclipped colour (reference dtype)   */
+  RTX_OUT_U8_HWC = 2   /* uint8  [n][3]  (255*clip(c,0,1)) truncated (base.py:147) */
+};
+
+#define RTX_UNBOUNDED (-1)       /* max_bounces: no cap, like the reference recursion */
+#define RTX_UNBOUNDED_LEVELS 333 /* ~ Python's recursion limit / 3 frames per level */
+#define RTX_FAST_MAX_BOUNCES 8   /* bounce caps served by the register-resident kernel */
+
+/* stats buffer (uint64 words, accumulated with atomics; pass NULL to disable) */
+enum {
+  RTX_S_PIXELS = 0,   /* rays started at level 0               */
+  RTX_S_DEFERRED = 1, /* rays handed to the general (tie/deep) kernel */
+  RTX_S_TIES = 2,     /* (ray, level) pairs with >1 nearest shape */
+  RTX_S_LEVELS = 64,  /* levels recorded                        */
+  RTX_S_RAYS = 8,     /* [8 .. 8+64): rays traced per level     */
+  RTX_S_HITS = 72,    /* [72 .. 72+64): shaded hits (= shadow rays) per level */
+  RTX_S_WORDS = 136
+};
+
+/* workspace: status words then deferred-ray list then per-worker frame stacks */
+enum {
+  RTX_WS_COUNT = 0,    /* uint32: deferred rays            */
+  RTX_WS_STATUS = 1,   /* uint32: RTX_ST_* flags           */
+  RTX_WS_HDR_BYTES = 256
+};
+enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2 };
+
+enum {
+  RTX_OK = 0,
+  RTX_E_ARG = -1,     /* bad argument (null pointer, size, kind)  */
+  RTX_E_LAUNCH = -2,  /* HIP launch / runtime error               */
+  RTX_E_WORKSPACE = -3 /* workspace too small                     */
+};
+
+/* Library version (RTX_ABI_VERSION) and the layout constants above, for the host to verify:
+ * writes up to n ints: {HDR_WORDS, GEOM_WORDS, MAT_WORDS, MAX_DOMES, S_WORDS, WS_HDR_BYTES,
+ * FAST_MAX_BOUNCES, UNBOUNDED_LEVELS}; returns RTX_ABI_VERSION. */
+int rtx_abi_version(int* layout, int n);
+const char* rtx_last_error(void);
+
+/* Bytes of workspace rtx_render_camera / rtx_trace_rays need for n rays at this bounce cap. */
+size_t rtx_workspace_bytes(int64_t n_rays, int max_bounces);
+
+/* Fused primary-ray generation + trace for the camera of `scene` (replaces
+ * get_ray_directions + raytrace_scene, base.py:91-141). Renders the local rows of one
+ * interleaved row tiling of the frame: local row lr is global row
+ *   ((lr / row_block) * n_parts + part) * row_block + lr % row_block,
+ * n_local_rows of them (1,1,0 with n_local_rows == height: the whole frame). Output holds
+ * n = width * n_local_rows pixels in local row-major order, as out_kind says. */
+int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
+                      int row_block, int n_parts, int part, int n_local_rows,
+                      int max_bounces, void* out, int out_kind,
+                      void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
+
+/* raytrace_scene(ray_origin, normalized_ray_direction, scene) for n rays (base.py:91-121),
+ * including all reflection levels up to max_bounces. origins: [3][n] (origin_stride == n) or one
+ * shared origin (origin_stride == 0, 3 doubles); dirs: [3][n]. */
+int rtx_trace_rays(const double* scene, int n_spheres, const double* origins, int64_t origin_stride,
+                   const double* dirs, int64_t n, int max_bounces, void* out, int out_kind,
+                   void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
+
+/* get_ray_directions (base.py:123-141) for the same row tiling: dirs_out [3][width*n_local_rows]. */
+int rtx_ray_directions(const double* scene, int width, int height, int row_block, int n_parts,
+                       int part, int n_local_rows, double* dirs_out, void* stream);
+
+/* NumpySphere.intersect (shape.py:28-51): t_out[i] = distance or 1e39 (FARAWAY).
+ * sphere: RTX_GEOM_WORDS doubles (cx, cy, cz, C.C, r*r, ...). */
+int rtx_sphere_intersect(const double* sphere, const double* origins, int64_t origin_stride,
+                         const double* dirs, int64_t n, double* t_out, void* stream);
+
+/* save_image's quantisation (base.py:143-151): color [3][n] (RTX_OUT_F32_SOA or _F64_SOA) ->
+ * out [n][3] uint8 = (uint8)(255 * clip(c, 0, 1)). */
+int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, void* stream);
+
+/* Live timing of the dominant render kernel (used by bench.py for the roofline): after
+ * rtx_profile_enable(k), the next k render launches record a hipEvent pair on their stream around
+ * k_render_fast (or k_render_general when it renders every ray). rtx_profile_collect waits for
+ * the recorded events and returns the summed kernel time and the launch count, then resets.
+ * rtx_profile_enable(0) disables. Not thread-safe; meant for benchmarks, not for graph capture. */
+int rtx_profile_enable(int max_launches);
+int rtx_profile_collect(double* total_ms, int* n_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTX_HIP_H */

@@ -1,0 +1,911 @@
+// rtx_kernels.hip — hand-written CDNA4 (gfx950) kernels for the python_ray_tracer render path,
+// plus the extern "C" entry points declared in include/rtx_hip.h.
+//
+// One thread = one ray (one pixel in camera mode); 64-lane waves cover 8x8 pixel tiles so the
+// rays of a wave stay coherent through the bounce chain. All geometry is float64 (SURVEY.md §7
+// hard part 1: the R=99999 ground sphere flips checker cells in fp32) and every expression keeps
+// the reference's operation order (file:line cited at each step); the library is compiled with
+// -ffp-contract=off because NumPy never fuses a multiply into an add.
+//
+// Kernels
+//   k_render_fast<B>  B <= RTX_FAST_MAX_BOUNCES. The reference's recursion
+//                     raytrace_scene -> create -> _calculate_reflection -> raytrace_scene
+//                     (base.py:91-121, shader.py:63-161) becomes an in-register loop over bounce
+//                     levels. The per-level shading terms (A, spec, g, irid) of the non-terminal
+//                     levels sit in a compile-time-sized shift register and are folded back from
+//                     the deepest level, reproducing the reference association
+//                         col_k = ((A_k + (spec_k + col_{k+1}*0.5)*g_k) + I_k)      (shader.py:106-110)
+//                     exactly. A ray that meets a tie (two shapes at the same nearest distance,
+//                     base.py:103 — both get shaded and summed) is appended to a deferred list.
+//   k_render_general  Any bounce cap, ties included: an explicit depth-first walk of the ray tree
+//                     with per-worker frame stacks in the workspace (HBM). Serves the deferred
+//                     list of k_render_fast, and every ray when B > RTX_FAST_MAX_BOUNCES.
+//   k_ray_dirs, k_intersect, k_quantize — the remaining boundary functions.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/rtx_hip.h"
+
+#define FARAWAY 1.0e39  // base.py:12
+#define RTX_PI 3.141592653589793  // np.pi
+
+namespace {
+
+constexpr int kBlock = 256;   // 4 waves
+constexpr int kTileW = 16;    // block tile: 16 x 16 pixels, each wave an 8 x 8 sub-tile
+constexpr int kTileH = 16;
+constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
+
+struct Params {
+  const double* scene;
+  int nsph;
+  int mode;  // 0: camera rays, 1: explicit rays
+  // camera mode
+  int width, height, row_block, n_parts, part, n_rows;
+  // explicit-ray mode
+  const double* org;
+  int64_t org_stride;
+  const double* dir;
+  // common
+  int64_t n;  // rays in this launch (= width * n_rows in camera mode)
+  int max_bounces;
+  void* out;
+  int out_kind;
+  uint8_t* ws;
+  int64_t list_cap;
+  double* stack;
+  int64_t n_workers;
+  int stack_levels;
+  unsigned long long* stats;
+};
+
+// ------------------------------------------------------------------------------------------
+// arithmetic helpers (reference semantics)
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ double dot3(double ax, double ay, double az, double bx, double by, double bz) {
+  return ((ax * bx) + (ay * by)) + (az * bz);  // NumpyVector3D.dot, base.py:34-35
+}
+
+__device__ __forceinline__ void norm3(double& x, double& y, double& z) {
+  // NumpyVector3D.norm, base.py:61-64: v * (1.0 / where(mag == 0, 1, mag))
+  const double mag = sqrt(dot3(x, y, z, x, y, z));
+  const double r = 1.0 / (mag == 0.0 ? 1.0 : mag);
+  x = x * r;
+  y = y * r;
+  z = z * r;
+}
+
+__device__ __forceinline__ double clip01(double x) {
+  // np.clip(x, 0, 1) (NaN propagates)
+  return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
+}
+
+__device__ __forceinline__ double max0(double x) {
+  // np.maximum(x, 0)
+  return x < 0.0 ? 0.0 : x;
+}
+
+__device__ __forceinline__ int trunc_parity(double x) {
+  // (x).astype(int) % 2 (shader.py:30): truncation to int64, then floor-mod 2 == (k & 1).
+  // |x| >= 2^53 doubles are even integers; NaN / |x| >= 2^63 convert to INT64_MIN (even).
+  const double k = trunc(x);
+  const double h = k * 0.5;
+  return (x == x) && (h != trunc(h));
+}
+
+// NumpySphere.intersect, shape.py:28-51, for a ray with precomputed oo = O.O.
+// b = 2 * D.(O - C);  c = ((C.C + O.O) - 2 * C.O) - r*r;  disc = b^2 - 4c.
+__device__ __forceinline__ double isect(const double* __restrict__ g, double ox, double oy, double oz, double oo,
+                                        double dx, double dy, double dz) {
+  const double cx = g[RTX_G_CX], cy = g[RTX_G_CY], cz = g[RTX_G_CZ];
+  const double b = 2.0 * dot3(dx, dy, dz, ox - cx, oy - cy, oz - cz);
+  const double c = ((g[RTX_G_CC] + oo) - 2.0 * dot3(cx, cy, cz, ox, oy, oz)) - g[RTX_G_RR];
+  const double disc = (b * b) - (4.0 * c);
+  double t = FARAWAY;
+  if (disc > 0.0) {  // np.where((disc > 0) & (sol > 0), sol, FARAWAY); sqrt(max(0, disc)) == sqrt(disc) here
+    const double sq = sqrt(disc);
+    const double s0 = (-b - sq) * 0.5;  // == / 2 exactly
+    const double s1 = (-b + sq) * 0.5;
+    const double sol = (s0 > 0.0 && s0 < s1) ? s0 : s1;
+    if (sol > 0.0) t = sol;
+  }
+  return t;
+}
+
+// Same, level-0 camera origin: O - C and c precomputed on the host with the same expressions.
+__device__ __forceinline__ double isect_cam(const double* __restrict__ g, double ocx, double ocy, double ocz,
+                                            double dx, double dy, double dz) {
+  const double b = 2.0 * dot3(dx, dy, dz, ocx, ocy, ocz);
+  const double disc = (b * b) - (4.0 * g[RTX_G_C0]);
+  double t = FARAWAY;
+  if (disc > 0.0) {
+    const double sq = sqrt(disc);
+    const double s0 = (-b - sq) * 0.5;
+    const double s1 = (-b + sq) * 0.5;
+    const double sol = (s0 > 0.0 && s0 < s1) ? s0 : s1;
+    if (sol > 0.0) t = sol;
+  }
+  return t;
+}
+
+// (x)^5 and (x)^2.5 for x in [0, 1] (shader.py:291, :310). NumPy evaluates these with its SIMD pow;
+// both are ~1 ulp, not correctly rounded, so neither side is "exact" here.
+__device__ __forceinline__ double pow5(double x) {
+  const double x2 = x * x;
+  return (x2 * x2) * x;
+}
+__device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt(x); }
+
+struct Shade {
+  double ar, ag, ab;  // ((0.004 + diffuse) + dome)           shader.py:86-98
+  double spec;        // physical specular (0 unless lit && g != 0: multiplied away otherwise)
+  double g;           // specular_gain
+  bool lit;           // shadow test                          shader.py:79-84
+  double ir, ig, ib;  // iridescence                          shader.py:110
+  double qx, qy, qz;  // nudged hit point (child ray origin)  shader.py:77
+  double nx, ny, nz;  // normal
+};
+
+// NumpyShader.create (shader.py:63-112) for one hit of sphere `h` at distance t, minus the
+// reflection recursion, which the caller drives. Returns with the normal in s.n*.
+__device__ __forceinline__ void shade_hit(const double* __restrict__ sc, const double* __restrict__ geo,
+                                          const double* __restrict__ mat, int nsph, int h, double ox, double oy,
+                                          double oz, double dx, double dy, double dz, double t, Shade& s) {
+  const double* gh = geo + h * RTX_GEOM_WORDS;
+  const double* mh = mat + h * RTX_MAT_WORDS;
+  const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73
+  const double inv_r = gh[RTX_G_INVR];
+  const double nx = (px - gh[RTX_G_CX]) * inv_r;  // :74 (not renormalised)
+  const double ny = (py - gh[RTX_G_CY]) * inv_r;
+  const double nz = (pz - gh[RTX_G_CZ]) * inv_r;
+  double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
+  norm3(lx, ly, lz);  // :75
+  double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
+  norm3(vx, vy, vz);  // :76 (towards the camera on every level)
+  const double qx = px + nx * 0.0001, qy = py + ny * 0.0001, qz = pz + nz * 0.0001;  // :77
+
+  // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
+  // Equivalent any-hit form: lit unless some sphere is strictly nearer than the shape itself.
+  const double qq = dot3(qx, qy, qz, qx, qy, qz);
+  const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
+  bool lit = true;
+  for (int j = 0; j < nsph; ++j) {
+    if (isect(geo + j * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz) < tself) {
+      lit = false;
+      break;
+    }
+  }
+  const double litf = lit ? 1.0 : 0.0;
+
+  // ambient + diffuse (:86-88, :130-141): 0.004 + ((tex * max(N.L, 0)) * lit) * diffuse_gain
+  const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));
+  double tr, tg, tb;
+  if (mh[RTX_M_TEX] != 0.0) {  // TextureChecker.get_color (:29-32)
+    const double c = (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0)) ? 1.0 : 0.0;
+    tr = tg = tb = c;
+  } else {  // Texture.get_color (:17-19)
+    tr = mh[RTX_M_TR];
+    tg = mh[RTX_M_TG];
+    tb = mh[RTX_M_TB];
+  }
+  const double dg = mh[RTX_M_DG];
+  double ar = 0.004 + ((tr * dli) * litf) * dg;
+  double ag = 0.004 + ((tg * dli) * litf) * dg;
+  double ab = 0.004 + ((tb * dli) * litf) * dg;
+
+  // dome light (:234-244): sum_i intensity_i * max(N.(0,1,0), 0), times the last dome colour
+  const double up = ((nx * 0.0) + (ny * 1.0)) + (nz * 0.0);
+  const int ndome = (int)sc[RTX_H_NDOME];
+  double di = 0.0;
+  for (int j = 0; j < ndome; ++j) di = di + sc[RTX_H_DOMEI + j] * max0(up);
+  ar = ar + sc[RTX_H_DOMEC + 0] * di;
+  ag = ag + sc[RTX_H_DOMEC + 1] * di;
+  ab = ab + sc[RTX_H_DOMEC + 2] * di;
+
+  // physical specular (:246-320). Only observable through (spec + 0.5 R) * g * lit (:106), so
+  // it is skipped when g == 0 or in shadow (finite * 0 == 0).
+  const double g = mh[RTX_M_G];
+  double spec = 0.0;
+  if (lit && g != 0.0) {
+    double Lx = lx, Ly = ly, Lz = lz;
+    norm3(Lx, Ly, Lz);  // :278 (normalised a second time)
+    double Vx = vx, Vy = vy, Vz = vz;
+    norm3(Vx, Vy, Vz);  // :279
+    double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
+    norm3(Hx, Hy, Hz);  // :280
+    const double NdotV = clip01(dot3(nx, ny, nz, Vx, Vy, Vz));  // :283
+    const double NdotH = clip01(dot3(nx, ny, nz, Hx, Hy, Hz));  // :284
+    const double VdotH = clip01(dot3(Vx, Vy, Vz, Hx, Hy, Hz));  // :285
+    const double NdotL = clip01(dot3(nx, ny, nz, Lx, Ly, Lz));  // :287
+    const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
+    const double a2 = mh[RTX_M_A2];
+    const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
+    const double D = a2 / (RTX_PI * ((denom * denom) + 1e-8));  // :296
+    const double oma2 = mh[RTX_M_1MA2];
+    const double G1L = (2.0 * NdotL) / ((NdotL + sqrt(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
+    const double G1V = (2.0 * NdotV) / ((NdotV + sqrt(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
+    const double G = G1L * G1V;  // :303
+    const double spec_base = ((F * D) * G) / ((4.0 * NdotV) + 1e-8);  // :306
+    const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
+    const double sf = spec_base + g * glint;  // :315
+    spec = (NdotV <= 0.0) ? 0.0 : sf;  // :318
+  }
+
+  // thin-film iridescence (:186-232); skipped when iridescence_gain == 0 (x * 0 == 0)
+  double ir = 0.0, ig = 0.0, ib = 0.0;
+  const double igain = mh[RTX_M_IG];
+  if (igain != 0.0) {
+    const double va = clip01(dot3(nx, ny, nz, vx, vy, vz));  // :201
+    const double af = fabs(va - 0.5) * 2.0;  // :204
+    const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
+    const double ip = sin(phase);  // :211
+    const double hs = mh[RTX_M_HS], omhs = mh[RTX_M_1MHS];
+    const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
+    const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222
+    const double b = 0.5 + 0.5 * ip;  // :223
+    const double w = mh[RTX_M_TFW];
+    ir = (r * w) * igain;  // :229-232
+    ig = (gg * w) * igain;
+    ib = (b * w) * igain;
+  }
+  s.ar = ar; s.ag = ag; s.ab = ab;
+  s.spec = spec;
+  s.g = g;
+  s.lit = lit;
+  s.ir = ir; s.ig = ig; s.ib = ib;
+  s.qx = qx; s.qy = qy; s.qz = qz;
+  s.nx = nx; s.ny = ny; s.nz = nz;
+}
+
+// Reflected direction (shader.py:151): norm(D - (N*2) * (D.N))
+__device__ __forceinline__ void reflect_dir(double& dx, double& dy, double& dz, double nx, double ny, double nz) {
+  const double dn = dot3(dx, dy, dz, nx, ny, nz);
+  double rx = dx - (nx * 2.0) * dn, ry = dy - (ny * 2.0) * dn, rz = dz - (nz * 2.0) * dn;
+  norm3(rx, ry, rz);
+  dx = rx;
+  dy = ry;
+  dz = rz;
+}
+
+// ------------------------------------------------------------------------------------------
+// ray setup / output
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ int global_row(const Params& p, int lr) {
+  return ((lr / p.row_block) * p.n_parts + p.part) * p.row_block + (lr % p.row_block);
+}
+
+// get_ray_directions (base.py:123-141) for pixel (col, global row r).
+__device__ __forceinline__ void camera_dir(const double* __restrict__ sc, int col, int r, int W, int H, double& dx,
+                                           double& dy, double& dz) {
+  // np.linspace: i*step + start, last element set to stop exactly
+  const double x = (sc[RTX_H_XFIX] != 0.0 && col == W - 1) ? sc[RTX_H_XSTOP]
+                                                            : (double)col * sc[RTX_H_XSTEP] + sc[RTX_H_XSTART];
+  const double y = (sc[RTX_H_YFIX] != 0.0 && r == H - 1) ? sc[RTX_H_YSTOP]
+                                                          : (double)r * sc[RTX_H_YSTEP] + sc[RTX_H_YSTART];
+  const double vx = x - sc[RTX_H_CAM + 0];
+  const double vy = y - sc[RTX_H_CAM + 1];
+  const double vz = sc[RTX_H_VZ];
+  const double mag = sqrt(((vx * vx) + (vy * vy)) + sc[RTX_H_VZ2]);
+  const double rr = 1.0 / (mag == 0.0 ? 1.0 : mag);
+  dx = vx * rr;
+  dy = vy * rr;
+  dz = vz * rr;
+}
+
+__device__ __forceinline__ void load_ray(const Params& p, int64_t i, double& ox, double& oy, double& oz, double& dx,
+                                         double& dy, double& dz) {
+  if (p.mode == 0) {
+    const int lr = (int)(i / p.width), col = (int)(i % p.width);
+    camera_dir(p.scene, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
+    ox = p.scene[RTX_H_CAM + 0];
+    oy = p.scene[RTX_H_CAM + 1];
+    oz = p.scene[RTX_H_CAM + 2];
+  } else {
+    const int64_t n = p.n;
+    dx = p.dir[i];
+    dy = p.dir[n + i];
+    dz = p.dir[2 * n + i];
+    const int64_t j = p.org_stride ? i : 0;
+    const int64_t s = p.org_stride;
+    ox = p.org[j];
+    oy = p.org[s + j + (s ? 0 : 1)];
+    oz = p.org[2 * s + j + (s ? 0 : 2)];
+  }
+}
+
+__device__ __forceinline__ unsigned char quant_u8(double c) {
+  // (255 * np.clip(c, 0, 1)).astype(np.uint8)  (base.py:147): truncation
+  const double v = 255.0 * clip01(c);
+  return (unsigned char)(int)v;
+}
+
+__device__ __forceinline__ void write_out(const Params& p, int64_t i, double r, double g, double b) {
+  if (p.out_kind == RTX_OUT_F32_SOA) {
+    float* o = (float*)p.out;
+    o[i] = (float)r;
+    o[p.n + i] = (float)g;
+    o[2 * p.n + i] = (float)b;
+  } else if (p.out_kind == RTX_OUT_F64_SOA) {
+    double* o = (double*)p.out;
+    o[i] = r;
+    o[p.n + i] = g;
+    o[2 * p.n + i] = b;
+  } else {
+    unsigned char* o = (unsigned char*)p.out + 3 * i;
+    o[0] = quant_u8(r);
+    o[1] = quant_u8(g);
+    o[2] = quant_u8(b);
+  }
+}
+
+__device__ __forceinline__ void stat_add(unsigned long long* st, int word, unsigned long long v) {
+  atomicAdd(st + word, v);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_render_fast<B>
+// ------------------------------------------------------------------------------------------
+
+template <int B>
+__global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
+  const double* __restrict__ sc = p.scene;
+  const double* __restrict__ geo = sc + RTX_HDR_WORDS;
+  const double* __restrict__ mat = geo + p.nsph * RTX_GEOM_WORDS;
+  const int nsph = p.nsph;
+
+  int64_t i;
+  if (p.mode == 0) {
+    // 16x16 block tile; wave w -> 8x8 sub-tile, lane -> (l & 7, l >> 3)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = blockIdx.x * kTileW + (w & 1) * 8 + (lane & 7);
+    const int lr = blockIdx.y * kTileH + (w >> 1) * 8 + (lane >> 3);
+    if (col >= p.width || lr >= p.n_rows) return;
+    i = (int64_t)lr * p.width + col;
+  } else {
+    i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.n) return;
+  }
+  double ox, oy, oz, dx, dy, dz;
+  load_ray(p, i, ox, oy, oz, dx, dy, dz);
+  const bool cam0 = (p.mode == 0);
+  unsigned long long* st = p.stats;
+  if (st) stat_add(st, RTX_S_PIXELS, 1);
+
+  constexpr int NS = B > 0 ? B : 1;
+  double sA[NS][3], sS[NS], sG[NS], sI[NS][3];
+  int depth = 0;
+  double cr = 0.0, cg = 0.0, cb = 0.0;
+  bool deferred = false;
+
+  for (int k = 0;; ++k) {
+    if (st && k < RTX_S_LEVELS) stat_add(st, RTX_S_RAYS + k, 1);
+    // nearest hit over all shapes (base.py:97-103)
+    double tmin = FARAWAY;
+    int hit = -1;
+    bool tie = false;
+    if (k == 0 && cam0) {
+      for (int s = 0; s < nsph; ++s) {
+        const double* gs = geo + s * RTX_GEOM_WORDS;
+        const double t = isect_cam(gs, ox - gs[RTX_G_CX], oy - gs[RTX_G_CY], oz - gs[RTX_G_CZ], dx, dy, dz);
+        if (t < tmin) {
+          tmin = t;
+          hit = s;
+          tie = false;
+        } else if (t == tmin && t != FARAWAY) {
+          tie = true;
+        }
+      }
+    } else {
+      const double oo = dot3(ox, oy, oz, ox, oy, oz);
+      for (int s = 0; s < nsph; ++s) {
+        const double t = isect(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
+        if (t < tmin) {
+          tmin = t;
+          hit = s;
+          tie = false;
+        } else if (t == tmin && t != FARAWAY) {
+          tie = true;
+        }
+      }
+    }
+    if (hit < 0) {  // nothing hit: NumpyRGBColor(0, 0, 0) (base.py:100)
+      cr = cg = cb = 0.0;
+      break;
+    }
+    if (tie) {  // several shapes shaded and summed: the general kernel takes this ray
+      deferred = true;
+      if (st) stat_add(st, RTX_S_TIES, 1);
+      break;
+    }
+    if (st && k < RTX_S_LEVELS) stat_add(st, RTX_S_HITS + k, 1);
+    Shade s;
+    shade_hit(sc, geo, mat, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+    const bool weighted = s.lit && s.g != 0.0;
+    if (!weighted || k >= B) {
+      // terminal level: reflection is black (capped) or multiplied by zero
+      const double t_r = weighted ? (s.spec + 0.0) * s.g : 0.0;
+      cr = (s.ar + t_r) + s.ir;
+      cg = (s.ag + t_r) + s.ig;
+      cb = (s.ab + t_r) + s.ib;
+      break;
+    }
+    // push this level's terms; the reflected ray becomes the next level
+#pragma unroll
+    for (int j = NS - 1; j > 0; --j) {
+      sA[j][0] = sA[j - 1][0]; sA[j][1] = sA[j - 1][1]; sA[j][2] = sA[j - 1][2];
+      sS[j] = sS[j - 1]; sG[j] = sG[j - 1];
+      sI[j][0] = sI[j - 1][0]; sI[j][1] = sI[j - 1][1]; sI[j][2] = sI[j - 1][2];
+    }
+    sA[0][0] = s.ar; sA[0][1] = s.ag; sA[0][2] = s.ab;
+    sS[0] = s.spec; sG[0] = s.g;
+    sI[0][0] = s.ir; sI[0][1] = s.ig; sI[0][2] = s.ib;
+    ++depth;
+    reflect_dir(dx, dy, dz, s.nx, s.ny, s.nz);
+    ox = s.qx;
+    oy = s.qy;
+    oz = s.qz;
+  }
+
+  if (deferred) {
+    uint32_t* hdr = (uint32_t*)p.ws;
+    const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
+    if ((int64_t)slot < p.list_cap) {
+      ((int64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = i;
+    } else {
+      atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
+    }
+    if (st) stat_add(st, RTX_S_DEFERRED, 1);
+    return;
+  }
+  // fold back (shader.py:106-110): col_k = ((A_k + (spec_k + col_{k+1}*0.5) * g_k) + I_k)
+  for (int d = 0; d < depth; ++d) {
+    cr = (sA[0][0] + (sS[0] + cr * 0.5) * sG[0]) + sI[0][0];
+    cg = (sA[0][1] + (sS[0] + cg * 0.5) * sG[0]) + sI[0][1];
+    cb = (sA[0][2] + (sS[0] + cb * 0.5) * sG[0]) + sI[0][2];
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j) {
+      sA[j][0] = sA[j + 1][0]; sA[j][1] = sA[j + 1][1]; sA[j][2] = sA[j + 1][2];
+      sS[j] = sS[j + 1]; sG[j] = sG[j + 1];
+      sI[j][0] = sI[j + 1][0]; sI[j][1] = sI[j + 1][1]; sI[j][2] = sI[j + 1][2];
+    }
+  }
+  write_out(p, i, cr, cg, cb);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_render_general: explicit depth-first ray tree (ties and any bounce cap)
+// ------------------------------------------------------------------------------------------
+
+// frame fields
+enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_TMIN, F_NEXT, F_AR, F_AG, F_AB,
+       F_PAR, F_PAG, F_PAB, F_PS, F_PG, F_PIR, F_PIG, F_PIB };
+
+struct Stack {
+  double* base;
+  int64_t nw;
+  int64_t w;
+  __device__ __forceinline__ double& at(int d, int f) const { return base[((int64_t)d * kFrameWords + f) * nw + w]; }
+};
+
+__device__ void trace_general(const Params& p, const Stack& S, double ox0, double oy0, double oz0, double dx0,
+                              double dy0, double dz0, double& cr, double& cg, double& cb) {
+  const double* __restrict__ sc = p.scene;
+  const double* __restrict__ geo = sc + RTX_HDR_WORDS;
+  const double* __restrict__ mat = geo + p.nsph * RTX_GEOM_WORDS;
+  const int nsph = p.nsph;
+  const int B = p.max_bounces;  // < 0: unbounded (bounded by the stack depth)
+  unsigned long long* st = p.stats;
+
+  S.at(0, F_OX) = ox0; S.at(0, F_OY) = oy0; S.at(0, F_OZ) = oz0;
+  S.at(0, F_DX) = dx0; S.at(0, F_DY) = dy0; S.at(0, F_DZ) = dz0;
+  S.at(0, F_NEXT) = -1.0;
+  int d = 0;
+  for (;;) {
+    const double ox = S.at(d, F_OX), oy = S.at(d, F_OY), oz = S.at(d, F_OZ);
+    const double dx = S.at(d, F_DX), dy = S.at(d, F_DY), dz = S.at(d, F_DZ);
+    const double oo = dot3(ox, oy, oz, ox, oy, oz);
+    int next = (int)S.at(d, F_NEXT);
+    double tmin;
+    if (next < 0) {  // new ray: nearest distance (base.py:97-98)
+      if (st && d < RTX_S_LEVELS) stat_add(st, RTX_S_RAYS + d, 1);
+      tmin = FARAWAY;
+      int nh = 0;
+      for (int s = 0; s < nsph; ++s) {
+        const double t = isect(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
+        if (t < tmin) {
+          tmin = t;
+          nh = 1;
+        } else if (t == tmin && t != FARAWAY) {
+          ++nh;
+        }
+      }
+      if (st && nh > 1) stat_add(st, RTX_S_TIES, 1);
+      S.at(d, F_TMIN) = tmin;
+      S.at(d, F_AR) = 0.0; S.at(d, F_AG) = 0.0; S.at(d, F_AB) = 0.0;  // NumpyRGBColor(0, 0, 0)
+      next = 0;
+    } else {
+      tmin = S.at(d, F_TMIN);
+    }
+    // next shape (scene order) with t == nearest (base.py:102-103)
+    int h = nsph;
+    if (tmin != FARAWAY) {
+      for (int s = next; s < nsph; ++s) {
+        if (isect(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz) == tmin) {
+          h = s;
+          break;
+        }
+      }
+    }
+    if (h == nsph) {  // this ray is done: its colour is the accumulated sum
+      const double rr = S.at(d, F_AR), rg = S.at(d, F_AG), rb = S.at(d, F_AB);
+      if (d == 0) {
+        cr = rr; cg = rg; cb = rb;
+        return;
+      }
+      --d;  // fold into the parent's pending hit (shader.py:106-110), then add (base.py:119)
+      const double pg = S.at(d, F_PG), ps = S.at(d, F_PS);
+      const double xr = (S.at(d, F_PAR) + (ps + rr * 0.5) * pg) + S.at(d, F_PIR);
+      const double xg = (S.at(d, F_PAG) + (ps + rg * 0.5) * pg) + S.at(d, F_PIG);
+      const double xb = (S.at(d, F_PAB) + (ps + rb * 0.5) * pg) + S.at(d, F_PIB);
+      S.at(d, F_AR) = S.at(d, F_AR) + xr;
+      S.at(d, F_AG) = S.at(d, F_AG) + xg;
+      S.at(d, F_AB) = S.at(d, F_AB) + xb;
+      S.at(d, F_NEXT) = S.at(d, F_NEXT) + 1.0;
+      continue;
+    }
+    if (st && d < RTX_S_LEVELS) stat_add(st, RTX_S_HITS + d, 1);
+    Shade s;
+    shade_hit(sc, geo, mat, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s);
+    const bool weighted = s.lit && s.g != 0.0;
+    bool descend = weighted && (B < 0 || d < B);
+    if (descend && d + 1 >= p.stack_levels) {  // deeper than the stack: RecursionError on the host
+      atomicOr((uint32_t*)p.ws + RTX_WS_STATUS, (uint32_t)RTX_ST_STACK_OVERFLOW);
+      descend = false;
+    }
+    if (!descend) {
+      const double t_r = weighted ? (s.spec + 0.0) * s.g : 0.0;
+      S.at(d, F_AR) = S.at(d, F_AR) + ((s.ar + t_r) + s.ir);
+      S.at(d, F_AG) = S.at(d, F_AG) + ((s.ag + t_r) + s.ig);
+      S.at(d, F_AB) = S.at(d, F_AB) + ((s.ab + t_r) + s.ib);
+      S.at(d, F_NEXT) = (double)(h + 1);
+      continue;
+    }
+    S.at(d, F_PAR) = s.ar; S.at(d, F_PAG) = s.ag; S.at(d, F_PAB) = s.ab;
+    S.at(d, F_PS) = s.spec; S.at(d, F_PG) = s.g;
+    S.at(d, F_PIR) = s.ir; S.at(d, F_PIG) = s.ig; S.at(d, F_PIB) = s.ib;
+    S.at(d, F_NEXT) = (double)h;
+    double rx = dx, ry = dy, rz = dz;
+    reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
+    ++d;
+    S.at(d, F_OX) = s.qx; S.at(d, F_OY) = s.qy; S.at(d, F_OZ) = s.qz;
+    S.at(d, F_DX) = rx; S.at(d, F_DY) = ry; S.at(d, F_DZ) = rz;
+    S.at(d, F_NEXT) = -1.0;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_render_general(Params p, int all_rays) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= p.n_workers) return;
+  const uint32_t* hdr = (const uint32_t*)p.ws;
+  int64_t count = all_rays ? p.n : (int64_t)hdr[RTX_WS_COUNT];
+  if (!all_rays && count > p.list_cap) count = p.list_cap;
+  const int64_t* list = (const int64_t*)(p.ws + RTX_WS_HDR_BYTES);
+  Stack S{p.stack, p.n_workers, w};
+  for (int64_t item = w; item < count; item += p.n_workers) {
+    const int64_t i = all_rays ? item : list[item];
+    double ox, oy, oz, dx, dy, dz;
+    load_ray(p, i, ox, oy, oz, dx, dy, dz);
+    if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
+    double cr, cg, cb;
+    trace_general(p, S, ox, oy, oz, dx, dy, dz, cr, cg, cb);
+    write_out(p, i, cr, cg, cb);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// boundary helpers
+// ------------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void k_ray_dirs(Params p, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= p.n) return;
+  const int lr = (int)(i / p.width), col = (int)(i % p.width);
+  double dx, dy, dz;
+  camera_dir(p.scene, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
+  out[i] = dx;
+  out[p.n + i] = dy;
+  out[2 * p.n + i] = dz;
+}
+
+__global__ __launch_bounds__(kBlock) void k_intersect(const double* __restrict__ g, const double* __restrict__ org,
+                                                      int64_t s, const double* __restrict__ dir, int64_t n,
+                                                      double* __restrict__ t) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t j = s ? i : 0;
+  const double ox = org[j], oy = org[s + j + (s ? 0 : 1)], oz = org[2 * s + j + (s ? 0 : 2)];
+  const double dx = dir[i], dy = dir[n + i], dz = dir[2 * n + i];
+  t[i] = isect(g, ox, oy, oz, dot3(ox, oy, oz, ox, oy, oz), dx, dy, dz);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_quantize(const T* __restrict__ c, int64_t n, uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  out[3 * i + 0] = quant_u8((double)c[i]);
+  out[3 * i + 1] = quant_u8((double)c[n + i]);
+  out[3 * i + 2] = quant_u8((double)c[2 * n + i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
+  snprintf(g_err, sizeof(g_err), fmt, a, b);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return RTX_E_LAUNCH;
+  }
+  return RTX_OK;
+}
+
+// Optional live timing of the dominant kernel (bench.py's roofline): a pool of event pairs recorded
+// on the launch stream around every k_render_fast (or k_render_general when it does all the work).
+struct Prof {
+  int cap = 0;
+  int used = 0;
+  hipEvent_t* ev = nullptr;  // 2 * cap
+} g_prof;
+
+void prof_free() {
+  for (int i = 0; i < 2 * g_prof.cap; ++i) hipEventDestroy(g_prof.ev[i]);
+  delete[] g_prof.ev;
+  g_prof = Prof{};
+}
+
+inline void prof_mark(int which, hipStream_t s) {
+  if (g_prof.cap && g_prof.used < g_prof.cap) hipEventRecord(g_prof.ev[2 * g_prof.used + which], s);
+}
+inline void prof_next() {
+  if (g_prof.cap && g_prof.used < g_prof.cap) ++g_prof.used;
+}
+
+int stack_levels_for(int max_bounces) {
+  return max_bounces < 0 ? RTX_UNBOUNDED_LEVELS : max_bounces + 1;
+}
+
+constexpr size_t kStackBudget = size_t(512) << 20;  // general-kernel frame stacks: <= 512 MiB
+constexpr int64_t kMaxWorkers = 65536;
+
+int64_t workers_for(int64_t n, int max_bounces) {
+  const size_t per = (size_t)stack_levels_for(max_bounces) * kFrameWords * sizeof(double);
+  int64_t w = (int64_t)(kStackBudget / per);
+  if (w > kMaxWorkers) w = kMaxWorkers;
+  const int64_t need = ((n + 63) / 64) * 64;
+  if (w > need) w = need;
+  w = (w / 64) * 64;
+  return w < 64 ? 64 : w;
+}
+
+size_t list_bytes(int64_t n) { return (size_t)n * sizeof(int64_t); }
+
+size_t ws_bytes(int64_t n, int max_bounces) {
+  const size_t stack = (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
+  return RTX_WS_HDR_BYTES + ((list_bytes(n) + 255) / 256) * 256 + stack;
+}
+
+template <int B>
+void launch_fast_b(const Params& p, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_render_fast<B>, grid, dim3(kBlock), 0, s, p);
+}
+
+void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
+  switch (B) {
+    case 0: launch_fast_b<0>(p, grid, s); break;
+    case 1: launch_fast_b<1>(p, grid, s); break;
+    case 2: launch_fast_b<2>(p, grid, s); break;
+    case 3: launch_fast_b<3>(p, grid, s); break;
+    case 4: launch_fast_b<4>(p, grid, s); break;
+    case 5: launch_fast_b<5>(p, grid, s); break;
+    case 6: launch_fast_b<6>(p, grid, s); break;
+    case 7: launch_fast_b<7>(p, grid, s); break;
+    default: launch_fast_b<8>(p, grid, s); break;
+  }
+}
+static_assert(RTX_FAST_MAX_BOUNCES == 8, "launch_fast switch covers 0..8");
+
+int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  if (p.nsph <= 0 || p.nsph > RTX_MAX_SPHERES) return fail(RTX_E_ARG, "n_spheres out of range%s (%lld)", "", p.nsph);
+  if (!p.scene || !p.out || !workspace) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (p.out_kind < 0 || p.out_kind > 2) return fail(RTX_E_ARG, "bad out_kind%s %lld", "", p.out_kind);
+  if (p.max_bounces < RTX_UNBOUNDED) return fail(RTX_E_ARG, "bad max_bounces%s %lld", "", p.max_bounces);
+  if (p.n <= 0) return RTX_OK;
+  const size_t need = ws_bytes(p.n, p.max_bounces);
+  if (workspace_bytes < need) return fail(RTX_E_WORKSPACE, "workspace too small%s (need %lld bytes)", "", (long long)need);
+  p.ws = (uint8_t*)workspace;
+  p.list_cap = p.n;
+  p.stack = (double*)(p.ws + RTX_WS_HDR_BYTES + ((list_bytes(p.n) + 255) / 256) * 256);
+  p.n_workers = workers_for(p.n, p.max_bounces);
+  p.stack_levels = stack_levels_for(p.max_bounces);
+  if (hipMemsetAsync(workspace, 0, RTX_WS_HDR_BYTES, s) != hipSuccess) return check_launch("hipMemsetAsync");
+  const bool fast = p.max_bounces >= 0 && p.max_bounces <= RTX_FAST_MAX_BOUNCES;
+  if (fast) {
+    dim3 grid;
+    if (p.mode == 0) {
+      grid = dim3((p.width + kTileW - 1) / kTileW, (p.n_rows + kTileH - 1) / kTileH);
+    } else {
+      grid = dim3((unsigned)((p.n + kBlock - 1) / kBlock));
+    }
+    prof_mark(0, s);
+    launch_fast(p.max_bounces, p, grid, s);
+    prof_mark(1, s);
+    prof_next();
+    if (int e = check_launch("k_render_fast")) return e;
+  } else {
+    prof_mark(0, s);
+  }
+  // deferred rays (ties) — or every ray when the cap is beyond the fast kernel
+  hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p, fast ? 0 : 1);
+  if (!fast) {
+    prof_mark(1, s);
+    prof_next();
+  }
+  return check_launch("k_render_general");
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+
+extern "C" {
+
+int rtx_abi_version(int* layout, int n) {
+  const int v[] = {RTX_HDR_WORDS, RTX_GEOM_WORDS, RTX_MAT_WORDS, RTX_MAX_DOMES, RTX_S_WORDS, RTX_WS_HDR_BYTES,
+                   RTX_FAST_MAX_BOUNCES, RTX_UNBOUNDED_LEVELS};
+  for (int i = 0; layout && i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) layout[i] = v[i];
+  return RTX_ABI_VERSION;
+}
+
+const char* rtx_last_error(void) { return g_err; }
+
+int rtx_profile_enable(int max_launches) {
+  prof_free();
+  if (max_launches <= 0) return RTX_OK;
+  g_prof.ev = new hipEvent_t[2 * (size_t)max_launches];
+  for (int i = 0; i < 2 * max_launches; ++i) {
+    if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) {
+      g_prof.cap = i / 2;
+      prof_free();
+      return fail(RTX_E_LAUNCH, "hipEventCreate failed%s", "");
+    }
+  }
+  g_prof.cap = max_launches;
+  return RTX_OK;
+}
+
+int rtx_profile_collect(double* total_ms, int* n_launches) {
+  double tot = 0.0;
+  for (int i = 0; i < g_prof.used; ++i) {
+    if (hipEventSynchronize(g_prof.ev[2 * i + 1]) != hipSuccess) return check_launch("hipEventSynchronize");
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]) != hipSuccess)
+      return check_launch("hipEventElapsedTime");
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (n_launches) *n_launches = g_prof.used;
+  g_prof.used = 0;
+  return RTX_OK;
+}
+
+size_t rtx_workspace_bytes(int64_t n_rays, int max_bounces) {
+  if (n_rays < 1) n_rays = 1;
+  if (max_bounces < RTX_UNBOUNDED) max_bounces = RTX_UNBOUNDED;
+  return ws_bytes(n_rays, max_bounces);
+}
+
+int rtx_render_camera(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
+                      int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
+                      size_t workspace_bytes, uint64_t* stats, void* stream) {
+  if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
+      n_local_rows < 0 || n_local_rows > height)
+    return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  Params p{};
+  p.scene = scene;
+  p.nsph = n_spheres;
+  p.mode = 0;
+  p.width = width;
+  p.height = height;
+  p.row_block = row_block;
+  p.n_parts = n_parts;
+  p.part = part;
+  p.n_rows = n_local_rows;
+  p.n = (int64_t)width * n_local_rows;
+  p.max_bounces = max_bounces;
+  p.out = out;
+  p.out_kind = out_kind;
+  p.stats = (unsigned long long*)stats;
+  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int rtx_trace_rays(const double* scene, int n_spheres, const double* origins, int64_t origin_stride,
+                   const double* dirs, int64_t n, int max_bounces, void* out, int out_kind, void* workspace,
+                   size_t workspace_bytes, uint64_t* stats, void* stream) {
+  if (!origins || !dirs) return fail(RTX_E_ARG, "null ray pointer%s", "");
+  if (origin_stride != 0 && origin_stride != n) return fail(RTX_E_ARG, "origin_stride must be 0 or n%s", "");
+  Params p{};
+  p.scene = scene;
+  p.nsph = n_spheres;
+  p.mode = 1;
+  p.org = origins;
+  p.org_stride = origin_stride;
+  p.dir = dirs;
+  p.n = n;
+  p.max_bounces = max_bounces;
+  p.out = out;
+  p.out_kind = out_kind;
+  p.stats = (unsigned long long*)stats;
+  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int rtx_ray_directions(const double* scene, int width, int height, int row_block, int n_parts, int part,
+                       int n_local_rows, double* dirs_out, void* stream) {
+  if (!scene || !dirs_out) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
+      n_local_rows < 0 || n_local_rows > height)
+    return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  Params p{};
+  p.scene = scene;
+  p.width = width;
+  p.height = height;
+  p.row_block = row_block;
+  p.n_parts = n_parts;
+  p.part = part;
+  p.n_rows = n_local_rows;
+  p.n = (int64_t)width * n_local_rows;
+  if (p.n == 0) return RTX_OK;
+  hipLaunchKernelGGL(k_ray_dirs, dim3((unsigned)((p.n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, p, dirs_out);
+  return check_launch("k_ray_dirs");
+}
+
+int rtx_sphere_intersect(const double* sphere, const double* origins, int64_t origin_stride, const double* dirs,
+                         int64_t n, double* t_out, void* stream) {
+  if (!sphere || !origins || !dirs || !t_out) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (origin_stride != 0 && origin_stride != n) return fail(RTX_E_ARG, "origin_stride must be 0 or n%s", "");
+  if (n <= 0) return RTX_OK;
+  hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
+                     sphere, origins, origin_stride, dirs, n, t_out);
+  return check_launch("k_intersect");
+}
+
+int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, void* stream) {
+  if (!color || !out) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (n <= 0) return RTX_OK;
+  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+  if (color_kind == RTX_OUT_F32_SOA) {
+    hipLaunchKernelGGL(k_quantize<float>, grid, dim3(kBlock), 0, (hipStream_t)stream, (const float*)color, n, out);
+  } else if (color_kind == RTX_OUT_F64_SOA) {
+    hipLaunchKernelGGL(k_quantize<double>, grid, dim3(kBlock), 0, (hipStream_t)stream, (const double*)color, n, out);
+  } else {
+    return fail(RTX_E_ARG, "bad color_kind%s %lld", "", color_kind);
+  }
+  return check_launch("k_quantize");
+}
+
+}  // extern "C"

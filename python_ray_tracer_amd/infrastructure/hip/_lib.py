@@ -1,0 +1,138 @@
+"""ctypes binding of the C ABI in ``include/rtx_hip.h`` (``librtx_hip.so``, built in-tree).
+
+There is no fallback: if the library is missing or was built for a different layout, importing the
+HIP backend raises. ``torch`` is imported first so the library binds to the HIP runtime torch has
+already loaded (one runtime per process; both are ``libamdhip64.so.7``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (loads the HIP runtime the library links against)
+
+PKG_DIR = Path(__file__).resolve().parent.parent.parent
+LIB_PATH = Path(os.environ.get("RTX_HIP_LIB", PKG_DIR / "librtx_hip.so"))
+
+# mirrors of include/rtx_hip.h (checked against the library at load time)
+ABI_VERSION = 1
+HDR_WORDS = 64
+GEOM_WORDS = 8
+MAT_WORDS = 24
+MAX_DOMES = 8
+S_WORDS = 136
+WS_HDR_BYTES = 256
+FAST_MAX_BOUNCES = 8
+UNBOUNDED_LEVELS = 333
+MAX_SPHERES = 1024
+MAGIC = 5527384.0
+UNBOUNDED = -1
+
+OUT_F32_SOA = 0
+OUT_F64_SOA = 1
+OUT_U8_HWC = 2
+
+ST_STACK_OVERFLOW = 1
+ST_LIST_OVERFLOW = 2
+
+# header words
+H_MAGIC, H_NSPH, H_CAM, H_LIGHT, H_DOMEC, H_NDOME, H_DOMEI = 0, 1, 2, 5, 8, 11, 12
+H_XSTART, H_XSTEP, H_XSTOP, H_XFIX = 20, 21, 22, 23
+H_YSTART, H_YSTEP, H_YSTOP, H_YFIX = 24, 25, 26, 27
+H_VZ, H_VZ2, H_W, H_H, H_CAMOO = 28, 29, 30, 31, 32
+# geometry words
+G_CX, G_CY, G_CZ, G_CC, G_RR, G_INVR, G_C0 = 0, 1, 2, 3, 4, 5, 6
+# material words
+(M_G, M_DG, M_TEX, M_TR, M_TG, M_TB, M_A2, M_A2M1, M_1MA2, M_F0, M_1MF0, M_IG, M_TFW, M_TFT, M_HS, M_1MHS,
+ M_ROUGH, M_REFL, M_IOR, M_TFIOR) = range(20)
+# stats words
+S_PIXELS, S_DEFERRED, S_TIES, S_RAYS, S_HITS, S_LEVELS = 0, 1, 2, 8, 72, 64
+
+EXPORTS = (
+    "rtx_abi_version",
+    "rtx_last_error",
+    "rtx_workspace_bytes",
+    "rtx_render_camera",
+    "rtx_trace_rays",
+    "rtx_ray_directions",
+    "rtx_sphere_intersect",
+    "rtx_quantize_u8",
+    "rtx_profile_enable",
+    "rtx_profile_collect",
+)
+
+_c_void_p = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_size = ctypes.c_size_t
+
+_SIGS = {
+    "rtx_abi_version": (_i32, [ctypes.POINTER(_i32), _i32]),
+    "rtx_last_error": (ctypes.c_char_p, []),
+    "rtx_workspace_bytes": (_size, [_i64, _i32]),
+    "rtx_render_camera": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
+                                 _c_void_p, _size, _c_void_p, _c_void_p]),
+    "rtx_trace_rays": (_i32, [_c_void_p, _i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i32, _c_void_p,
+                              _size, _c_void_p, _c_void_p]),
+    "rtx_ray_directions": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "rtx_sphere_intersect": (_i32, [_c_void_p, _c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "rtx_quantize_u8": (_i32, [_c_void_p, _i32, _i64, _c_void_p, _c_void_p]),
+    "rtx_profile_enable": (_i32, [_i32]),
+    "rtx_profile_collect": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
+}
+
+_lib = None
+
+
+class RtxError(RuntimeError):
+    """A C-ABI entry point returned an error code."""
+
+
+def load():
+    """Load and check ``librtx_hip.so``; raises (ImportError/RuntimeError) if unusable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"librtx_hip.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the HIP backend has no CPU fallback)")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    layout = (_i32 * 8)()
+    ver = lib.rtx_abi_version(layout, 8)
+    want = [HDR_WORDS, GEOM_WORDS, MAT_WORDS, MAX_DOMES, S_WORDS, WS_HDR_BYTES, FAST_MAX_BOUNCES, UNBOUNDED_LEVELS]
+    if ver != ABI_VERSION or list(layout) != want:
+        raise ImportError(f"librtx_hip.so ABI mismatch: version {ver}, layout {list(layout)} != {want}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _lib.rtx_last_error().decode(errors="replace") if _lib is not None else ""
+        raise RtxError(f"{what} failed ({rc}): {msg}")
+
+
+def profile_enable(max_launches: int) -> None:
+    check(load().rtx_profile_enable(int(max_launches)), "rtx_profile_enable")
+
+
+def profile_collect() -> tuple[float, int]:
+    """(summed ms of the dominant render kernel, launches) since profile_enable; synchronises."""
+    ms = ctypes.c_double()
+    n = _i32()
+    check(load().rtx_profile_collect(ctypes.byref(ms), ctypes.byref(n)), "rtx_profile_collect")
+    return ms.value, n.value
+
+
+def stream_handle(stream=None) -> int:
+    """hipStream_t of a torch stream (default: the current stream of the current device)."""
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)

@@ -1,0 +1,386 @@
+"""HIP backend: vector containers and ``HipRenderer``, the drop-in for ``NumpyRenderer``.
+
+Reference surface (``/root/reference/ray_tracer/infrastructure/numpy/base.py``):
+
+* ``FARAWAY``                                  — ``base.py:12``
+* ``NumpyVector3D`` / ``NumpyVectorArray3D`` / ``NumpyRGBColor`` — ``base.py:28-87``
+  -> ``HipVector3D`` / ``HipVectorArray3D`` / ``HipRGBColor``: the same SoA container, whose
+  components may be Python scalars, NumPy arrays or device tensors. The algebra (``dot``, ``norm``,
+  ``extract``, ``place`` …) keeps the reference semantics for API compatibility; it is convenience,
+  not the hot path — the renderer never computes through it.
+* ``NumpyRenderer``                            — ``base.py:90-151`` -> ``HipRenderer``:
+  ``get_ray_directions`` returns a lazy ``HipCameraRays`` batch; ``raytrace_scene`` on that batch
+  launches one fused kernel (ray generation + all bounce levels, ``rtx_render_camera``); on any other
+  rays it launches ``rtx_trace_rays``; ``save_image`` quantises on the device
+  (``rtx_quantize_u8``) and writes the PNG with Pillow like ``base.py:143-151``.
+
+Differences from the reference, all deliberate and documented in DESIGN.md:
+* ``HipRenderer(max_bounces=None)`` (the default) follows the reference's unbounded recursion up to
+  ``UNBOUNDED_LEVELS`` (333) levels and raises ``RecursionError`` beyond, where Python's recursion
+  limit would stop the reference. ``max_bounces=B`` caps it (levels 0..B shaded, level B+1 black).
+* ``color_dtype`` float64 (default, the reference dtype) or float32.
+"""
+
+from __future__ import annotations
+
+import numbers
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from python_ray_tracer_amd.application import Renderer
+from python_ray_tracer_amd.domain import Camera, RGBColor, Vector3D
+
+from . import _lib as L
+from .scene_pack import blob_key, camera_words, pack_scene
+
+FARAWAY = 1.0e39  # base.py:12
+
+
+def _is_tensor(x) -> bool:
+    return isinstance(x, torch.Tensor)
+
+
+def _sqrt(x):
+    return torch.sqrt(x) if _is_tensor(x) else np.sqrt(x)
+
+
+def _where(c, a, b):
+    if _is_tensor(c):
+        return torch.where(c, torch.as_tensor(a, dtype=torch.float64, device=c.device),
+                           torch.as_tensor(b, dtype=torch.float64, device=c.device) if not _is_tensor(b) else b)
+    return np.where(c, a, b)
+
+
+class HipVector3D(Vector3D):
+    """SoA 3-vector (reference ``NumpyVector3D``, base.py:28-79)."""
+
+    def __init__(self, x, y, z) -> None:
+        (self.x, self.y, self.z) = (x, y, z)
+
+    def dot(self, other):
+        return (self.x * other.x) + (self.y * other.y) + (self.z * other.z)  # base.py:34-35
+
+    def __abs__(self):
+        return self.dot(self)  # squared norm, base.py:37-38
+
+    def components(self):
+        return (self.x, self.y, self.z)
+
+    def __mul__(self, other):
+        if isinstance(other, HipVector3D):
+            return HipVector3D(self.x * other.x, self.y * other.y, self.z * other.z)
+        return HipVector3D(self.x * other, self.y * other, self.z * other)
+
+    def __add__(self, other):
+        return HipVector3D(self.x + other.x, self.y + other.y, self.z + other.z)
+
+    def __sub__(self, other):
+        return HipVector3D(self.x - other.x, self.y - other.y, self.z - other.z)
+
+    def __neg__(self):
+        return HipVector3D(-self.x, -self.y, -self.z)
+
+    def __truediv__(self, other):
+        return HipVector3D(self.x / other, self.y / other, self.z / other)
+
+    def norm(self):
+        mag = _sqrt(self.dot(self))  # base.py:61-64
+        return self * (1.0 / _where(mag == 0, 1, mag))
+
+    def extract(self, cond):
+        if isinstance(cond, numbers.Number):
+            return self
+        return HipVectorArray3D(*(_extract(cond, c) for c in self.components()))
+
+    def place(self, cond):
+        out = []
+        for c in self.components():
+            if _is_tensor(cond):
+                r = torch.zeros(cond.shape, dtype=torch.float64, device=cond.device)
+                r[cond] = torch.as_tensor(c, dtype=torch.float64, device=cond.device)
+            else:
+                r = np.zeros(np.shape(cond))
+                np.place(r, cond, c)
+            out.append(r)
+        return HipVector3D(*out)
+
+    # --- device helpers -------------------------------------------------------------------
+    def is_scalar(self) -> bool:
+        return all(np.ndim(c) == 0 and not (_is_tensor(c) and c.dim() > 0) for c in self.components())
+
+    def to_tensor(self, device, n: int | None = None) -> torch.Tensor:
+        """[3] (shared/scalar) or [3, n] float64 contiguous device tensor."""
+        comps = self.components()
+        if self.is_scalar():
+            vals = [float(c) for c in comps]
+            return torch.tensor(vals, dtype=torch.float64).to(device)
+        cols = []
+        for c in comps:
+            t = c if _is_tensor(c) else torch.from_numpy(np.ascontiguousarray(np.asarray(c, dtype=np.float64)))
+            t = t.to(device=device, dtype=torch.float64)
+            cols.append(t.reshape(-1) if t.dim() else t.expand(n if n is not None else 1))
+        length = max(int(c.numel()) for c in cols)
+        cols = [c.expand(length) if c.numel() == 1 else c for c in cols]
+        return torch.stack(cols).contiguous()
+
+    def numpy(self):
+        return tuple(c.detach().cpu().numpy() if _is_tensor(c) else np.asarray(c) for c in self.components())
+
+
+def _extract(cond, x):
+    if isinstance(x, numbers.Number):
+        return x
+    if _is_tensor(x):
+        return x[cond]
+    return np.extract(cond, x)
+
+
+class HipVectorArray3D(HipVector3D):
+    """Reference ``NumpyVectorArray3D`` (base.py:82-83)."""
+
+
+class HipRGBColor(HipVector3D, RGBColor):
+    """Reference ``NumpyRGBColor`` (base.py:86-87). ``HipRenderer`` returns one backed by a single
+    ``[3, n]`` device tensor (``.data``); ``.x/.y/.z`` are its rows."""
+
+    @classmethod
+    def from_tensor(cls, t: torch.Tensor) -> HipRGBColor:
+        c = cls(t[0], t[1], t[2])
+        c.data = t
+        return c
+
+
+class HipCameraRays(HipVectorArray3D):
+    """Lazy result of ``HipRenderer.get_ray_directions`` (base.py:123-141).
+
+    ``raytrace_scene`` on this batch never materialises it: ray generation is fused into the render
+    kernel. Reading ``.x/.y/.z`` materialises the float64 ``[3, W*H]`` tensor on the device (the exact
+    ``np.linspace`` / ``norm`` arithmetic of the reference)."""
+
+    def __init__(self, renderer: HipRenderer, camera: Camera) -> None:  # noqa: D107
+        self._renderer = renderer
+        self.camera = camera
+        self._data = None
+
+    def _materialise(self) -> torch.Tensor:
+        if self._data is None:
+            self._data = self._renderer._ray_directions(self.camera)
+        return self._data
+
+    @property
+    def data(self) -> torch.Tensor:
+        return self._materialise()
+
+    x = property(lambda self: self._materialise()[0])
+    y = property(lambda self: self._materialise()[1])
+    z = property(lambda self: self._materialise()[2])
+
+
+_OUT_KIND = {torch.float32: L.OUT_F32_SOA, torch.float64: L.OUT_F64_SOA}
+
+
+class HipRenderer(Renderer):
+    """MI355X renderer behind the reference ``Renderer`` plugin surface (application.py:7-32)."""
+
+    def __init__(self, max_bounces: int | None = None, *, color_dtype: torch.dtype = torch.float64,
+                 device=None, collect_stats: bool = False) -> None:
+        self._lib = L.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("HipRenderer needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")
+        if max_bounces is not None and (int(max_bounces) != max_bounces or max_bounces < 0):
+            raise ValueError(f"max_bounces must be None or a non-negative int, got {max_bounces!r}")
+        if color_dtype not in _OUT_KIND:
+            raise ValueError(f"color_dtype must be float32 or float64, got {color_dtype}")
+        self.max_bounces = None if max_bounces is None else int(max_bounces)
+        self.color_dtype = color_dtype
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self._scene_cache: dict = {}
+        self._ws = None
+        self.stats_buffer = torch.zeros(L.S_WORDS, dtype=torch.int64, device=self.device) if collect_stats else None
+
+    # ---------------------------------------------------------------- plumbing
+    @property
+    def _bounces_arg(self) -> int:
+        return L.UNBOUNDED if self.max_bounces is None else self.max_bounces
+
+    def _stream(self) -> int:
+        return L.stream_handle(torch.cuda.current_stream(self.device))
+
+    def scene_blob(self, scene) -> tuple[torch.Tensor, int]:
+        """Packed scene on the device (cached by content)."""
+        blob = pack_scene(scene)
+        key = blob_key(blob)
+        t = self._scene_cache.get(key)
+        if t is None:
+            t = torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True)
+            if len(self._scene_cache) >= 16:
+                self._scene_cache.pop(next(iter(self._scene_cache)))
+            self._scene_cache[key] = t
+        return t, int(blob[L.H_NSPH])
+
+    def workspace(self, n: int) -> torch.Tensor:
+        need = int(self._lib.rtx_workspace_bytes(int(n), self._bounces_arg))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _stats_ptr(self):
+        return None if self.stats_buffer is None else self.stats_buffer.data_ptr()
+
+    def _check_status(self, ws: torch.Tensor) -> None:
+        if self.max_bounces is None or self.max_bounces > L.FAST_MAX_BOUNCES:
+            status = int(ws[:8].view(torch.int32)[1].item())
+            if status & L.ST_STACK_OVERFLOW:
+                raise RecursionError(f"maximum recursion depth exceeded (reflection chain > {L.UNBOUNDED_LEVELS} levels)")
+
+    # ---------------------------------------------------------------- Renderer API
+    def get_ray_directions(self, camera: Camera) -> HipCameraRays:
+        """base.py:123-141 — lazy; see HipCameraRays."""
+        camera_words((float(camera.position.x), float(camera.position.y), float(camera.position.z)),
+                     camera.width, camera.height)  # validate now, like the reference would fail now
+        return HipCameraRays(self, camera)
+
+    def raytrace_scene(self, ray_origin: Vector3D, normalized_ray_direction: Vector3D, scene) -> HipRGBColor:
+        """base.py:91-121 including every reflection level (shader.py:143-161)."""
+        if isinstance(normalized_ray_direction, HipCameraRays) and normalized_ray_direction._data is None:
+            cam = normalized_ray_direction.camera
+            if _same_camera(cam, scene.camera) and _same_point(ray_origin, cam.position):
+                return HipRGBColor.from_tensor(self.render_tile(scene))
+        return HipRGBColor.from_tensor(self._trace(ray_origin, normalized_ray_direction, scene))
+
+    def save_image(self, color, camera: Camera, output_path) -> None:
+        """base.py:143-151: per channel (255*clip(c,0,1)).astype(uint8), reshaped (H, W), PNG."""
+        hwc = self.quantize(color, camera)
+        _write_png(hwc.cpu().numpy(), output_path)
+
+    # ---------------------------------------------------------------- extensions
+    def render(self, scene) -> HipRGBColor:
+        """get_ray_directions + raytrace_scene of the scene camera (application.py:48-50), fused."""
+        return HipRGBColor.from_tensor(self.render_tile(scene))
+
+    def render_tile(self, scene, row_block: int = 1, n_parts: int = 1, part: int = 0, out: str | None = None,
+                    blob: torch.Tensor | None = None, n_spheres: int | None = None) -> torch.Tensor:
+        """Render the interleaved row tile ``part`` of ``n_parts`` (row blocks of ``row_block``) of
+        the scene camera's frame. Returns [3, rows*W] colour (``out=None``) or [rows, W, 3] uint8
+        (``out="u8"``), rows in local order (python_ray_tracer_amd.tiling.tile_rows)."""
+        from python_ray_tracer_amd.tiling import n_local_rows
+
+        cam = scene.camera
+        W, H = int(cam.width), int(cam.height)
+        if blob is None:
+            blob, n_spheres = self.scene_blob(scene)
+        rows = n_local_rows(H, row_block, n_parts, part)
+        n = W * rows
+        if out == "u8":
+            res = torch.empty((rows, W, 3), dtype=torch.uint8, device=self.device)
+            kind = L.OUT_U8_HWC
+        else:
+            res = torch.empty((3, n), dtype=self.color_dtype, device=self.device)
+            kind = _OUT_KIND[self.color_dtype]
+        ws = self.workspace(n)
+        L.check(self._lib.rtx_render_camera(blob.data_ptr(), n_spheres, W, H, row_block, n_parts, part, rows,
+                                            self._bounces_arg, res.data_ptr(), kind, ws.data_ptr(), ws.numel(),
+                                            self._stats_ptr(), self._stream()), "rtx_render_camera")
+        self._check_status(ws)
+        return res
+
+    def _trace(self, ray_origin, dirs, scene) -> torch.Tensor:
+        blob, S = self.scene_blob(scene)
+        D = _as_vector(dirs).to_tensor(self.device)
+        if D.dim() != 2:
+            D = D.reshape(3, 1)
+        n = D.shape[1]
+        O = _as_vector(ray_origin).to_tensor(self.device, n)
+        stride = 0 if O.dim() == 1 else n
+        if stride and O.shape[1] != n:
+            raise ValueError(f"origins ({O.shape[1]}) and directions ({n}) differ in length")
+        res = torch.empty((3, n), dtype=self.color_dtype, device=self.device)
+        ws = self.workspace(n)
+        L.check(self._lib.rtx_trace_rays(blob.data_ptr(), S, O.data_ptr(), stride, D.data_ptr(), n,
+                                         self._bounces_arg, res.data_ptr(), _OUT_KIND[self.color_dtype],
+                                         ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream()),
+                "rtx_trace_rays")
+        self._check_status(ws)
+        return res
+
+    def _ray_directions(self, camera: Camera) -> torch.Tensor:
+        # a camera-only blob: no shapes needed for ray generation
+        pos = (float(camera.position.x), float(camera.position.y), float(camera.position.z))
+        blob = np.zeros(L.HDR_WORDS, dtype=np.float64)
+        cw = camera_words(pos, camera.width, camera.height)
+        blob[L.H_CAM:L.H_CAM + 3] = pos
+        blob[L.H_XSTART], blob[L.H_XSTEP], blob[L.H_XSTOP], blob[L.H_XFIX] = cw["xs"]
+        blob[L.H_YSTART], blob[L.H_YSTEP], blob[L.H_YSTOP], blob[L.H_YFIX] = cw["ys"]
+        blob[L.H_VZ], blob[L.H_VZ2] = cw["vz"], cw["vz2"]
+        dev_blob = torch.from_numpy(blob).to(self.device)
+        W, H = int(camera.width), int(camera.height)
+        out = torch.empty((3, W * H), dtype=torch.float64, device=self.device)
+        L.check(self._lib.rtx_ray_directions(dev_blob.data_ptr(), W, H, 1, 1, 0, H, out.data_ptr(), self._stream()),
+                "rtx_ray_directions")
+        return out
+
+    def quantize(self, color, camera: Camera) -> torch.Tensor:
+        """Device-side ``(255*clip(c,0,1)).astype(uint8)`` -> [H, W, 3] uint8 (base.py:145-149)."""
+        W, H = int(camera.width), int(camera.height)
+        t = color.data if isinstance(color, HipRGBColor) and hasattr(color, "data") else _as_vector(color).to_tensor(self.device)
+        if t.dim() == 1:
+            t = t.reshape(3, 1)
+        if t.dtype not in _OUT_KIND:
+            t = t.to(torch.float64)
+        t = t.contiguous()
+        n = t.shape[1]
+        if n != W * H:
+            # np.reshape in save_image (base.py:147)
+            raise ValueError(f"cannot reshape array of size {n} into shape ({H},{W})")
+        out = torch.empty((H, W, 3), dtype=torch.uint8, device=self.device)
+        L.check(self._lib.rtx_quantize_u8(t.data_ptr(), _OUT_KIND[t.dtype], n, out.data_ptr(), self._stream()),
+                "rtx_quantize_u8")
+        return out
+
+    def stats(self) -> dict:
+        """Per-level counters accumulated since construction / reset_stats (synchronises)."""
+        if self.stats_buffer is None:
+            raise RuntimeError("construct HipRenderer(collect_stats=True) to count rays")
+        s = self.stats_buffer.cpu().tolist()
+        rays = s[L.S_RAYS:L.S_RAYS + L.S_LEVELS]
+        hits = s[L.S_HITS:L.S_HITS + L.S_LEVELS]
+        last = max([i + 1 for i, v in enumerate(rays) if v] or [0])
+        return {"pixels": s[L.S_PIXELS], "deferred": s[L.S_DEFERRED], "ties": s[L.S_TIES],
+                "rays": rays[:last], "hits": hits[:last]}
+
+    def reset_stats(self) -> None:
+        if self.stats_buffer is not None:
+            self.stats_buffer.zero_()
+
+
+def _as_vector(v) -> HipVector3D:
+    if isinstance(v, HipVector3D):
+        return v
+    if isinstance(v, torch.Tensor) and v.dim() >= 1 and v.shape[0] == 3:
+        return HipVector3D(v[0], v[1], v[2])
+    if hasattr(v, "x") and hasattr(v, "y") and hasattr(v, "z"):
+        return HipVector3D(v.x, v.y, v.z)
+    raise TypeError(f"expected a 3-vector, got {type(v).__name__}")
+
+
+def _same_point(a, b) -> bool:
+    try:
+        return all(np.ndim(u) == 0 and float(u) == float(w) for u, w in zip(_as_vector(a).components(),
+                                                                            _as_vector(b).components()))
+    except TypeError:
+        return False
+
+
+def _same_camera(a: Camera, b: Camera) -> bool:
+    return a is b or (int(a.width) == int(b.width) and int(a.height) == int(b.height)
+                      and _same_point(a.position, b.position))
+
+
+def _write_png(hwc: np.ndarray, output_path) -> None:
+    from PIL import Image
+
+    # base.py:145-151 builds three "L" images and merges them into "RGB": same pixels.
+    img = Image.fromarray(np.ascontiguousarray(hwc, dtype=np.uint8))
+    img.save(output_path if hasattr(output_path, "write") else Path(output_path))

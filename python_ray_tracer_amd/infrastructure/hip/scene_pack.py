@@ -1,0 +1,163 @@
+"""Scene packer: ``Scene3D`` -> one float64 blob (layout: ``include/rtx_hip.h``).
+
+Everything the reference reads from the scene during a render is flattened
+here, once per scene/camera, and uploaded (≈10 KB). Per-material constants that the reference
+evaluates in Python scalar arithmetic (``alpha = roughness**2``, ``F0``, the thin-film hue shift,
+``1.0/radius``, ``|C|^2``, the level-0 camera terms of ``shape.py:35-37`` …) are evaluated here with
+the very same Python expressions, so they are bit-identical to what the reference computes.
+
+Duck-typed: works with this package's ``HipSphere``/``HipShader`` and with the reference's own
+``NumpySphere``/``NumpyShader`` objects (same attribute names), so an existing reference scene
+renders unchanged.
+"""
+
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _xyz(v):
+    return float(v.x), float(v.y), float(v.z)
+
+
+def _linspace_params(start, stop, num: int):
+    """np.linspace(start, stop, num) as (start, step, stop, fix_last): y_i = i*step + start and,
+    when num > 1, the last element is set to stop exactly (numpy/_core/function_base.py)."""
+    start = float(start)
+    stop = float(stop)
+    div = num - 1
+    if div > 0:
+        step = (stop - start) / div
+        if step == 0:
+            raise NotImplementedError("np.linspace denormal-step branch is not supported")
+        return start, step, stop, 1.0
+    return start, 0.0, stop, 0.0
+
+
+def camera_words(position, width: int, height: int) -> dict:
+    """get_ray_directions' screen (base.py:123-141) as kernel parameters."""
+    if int(width) <= 0 or int(height) <= 0:
+        raise ValueError(f"camera size must be positive, got {width}x{height}")
+    aspect_ratio = float(width) / height
+    screen = (-1, 1 / aspect_ratio + 0.25, 1, -1 / aspect_ratio + 0.25)
+    xs = _linspace_params(screen[0], screen[2], int(width))
+    ys = _linspace_params(screen[1], screen[3], int(height))
+    cx, cy, cz = position
+    vz = 0 - cz
+    return {"xs": xs, "ys": ys, "vz": vz, "vz2": vz * vz, "oo": (cx * cx + cy * cy) + cz * cz}
+
+
+def _shape_fields(shape):
+    if hasattr(shape, "texture"):
+        # NumpyTexturedSphere (shape.py:57-90) passes an RGB colour as its shader and cannot render
+        # in the reference either (base.py:110); image textures are out of scope.
+        raise NotImplementedError("image-textured spheres are not supported (reference NumpyTexturedSphere is broken)")
+    pos = getattr(shape, "position", None) or getattr(shape, "center", None)
+    if pos is None or not hasattr(shape, "radius") or not hasattr(shape, "shader"):
+        raise TypeError(f"HipRenderer renders spheres only; got {type(shape).__name__}")
+    return _xyz(pos), shape.radius, shape.shader
+
+
+def pack_scene(scene) -> np.ndarray:
+    """Flatten ``scene`` (shapes, lights, camera) into the float64 blob of include/rtx_hip.h."""
+    shapes = list(scene.shapes)
+    S = len(shapes)
+    if S == 0:
+        # reduce(np.minimum, []) in NumpyRenderer.raytrace_scene (base.py:98)
+        raise TypeError("reduce() of empty iterable with no initial value")
+    if S > L.MAX_SPHERES:
+        raise ValueError(f"at most {L.MAX_SPHERES} spheres per scene, got {S}")
+    lights = list(scene.lights)
+    light0 = lights[0]  # IndexError like shader.py:75 when the scene has no light
+    lpos = light0.position  # AttributeError like shader.py:75 when lights[0] is a DomeLight
+    domes = [li for li in lights if type(li).__name__ == "DomeLight"]
+    if len(domes) > L.MAX_DOMES:
+        raise ValueError(f"at most {L.MAX_DOMES} DomeLights, got {len(domes)}")
+    cam = scene.camera
+    cpos = _xyz(cam.position)
+    W, H = int(cam.width), int(cam.height)
+
+    blob = np.zeros(L.HDR_WORDS + S * (L.GEOM_WORDS + L.MAT_WORDS), dtype=np.float64)
+    h = blob[: L.HDR_WORDS]
+    h[L.H_MAGIC] = L.MAGIC
+    h[L.H_NSPH] = S
+    h[L.H_CAM:L.H_CAM + 3] = cpos
+    h[L.H_LIGHT:L.H_LIGHT + 3] = _xyz(lpos)
+    dome_color = (1.0, 1.0, 1.0)  # shader.py:237
+    for i, d in enumerate(domes):
+        dome_color = _xyz(d.color)  # the last DomeLight's colour wins (shader.py:241)
+        h[L.H_DOMEI + i] = float(d.intensity)
+    h[L.H_DOMEC:L.H_DOMEC + 3] = dome_color
+    h[L.H_NDOME] = len(domes)
+    cw = camera_words(cpos, W, H)
+    h[L.H_XSTART], h[L.H_XSTEP], h[L.H_XSTOP], h[L.H_XFIX] = cw["xs"]
+    h[L.H_YSTART], h[L.H_YSTEP], h[L.H_YSTOP], h[L.H_YFIX] = cw["ys"]
+    h[L.H_VZ], h[L.H_VZ2] = cw["vz"], cw["vz2"]
+    h[L.H_W], h[L.H_H] = W, H
+    h[L.H_CAMOO] = cw["oo"]
+    ox, oy, oz = cpos
+
+    geo = blob[L.HDR_WORDS: L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
+    mat = blob[L.HDR_WORDS + S * L.GEOM_WORDS:].reshape(S, L.MAT_WORDS)
+    for s, shape in enumerate(shapes):
+        (cx, cy, cz), radius, sh = _shape_fields(shape)
+        cc = (cx * cx + cy * cy) + cz * cz  # abs(self.position), shape.py:35
+        rr = radius * radius  # shape.py:36
+        co = (cx * ox + cy * oy) + cz * oz
+        geo[s, L.G_CX:L.G_CZ + 1] = (cx, cy, cz)
+        geo[s, L.G_CC] = cc
+        geo[s, L.G_RR] = rr
+        geo[s, L.G_INVR] = 1.0 / radius  # shader.py:74
+        geo[s, L.G_C0] = ((cc + cw["oo"]) - 2 * co) - rr  # shape.py:35-37 with the camera origin
+
+        tex = sh.diffuse_color
+        m = mat[s]
+        m[L.M_G] = sh.specular_gain
+        m[L.M_DG] = sh.diffuse_gain
+        if type(tex).__name__ == "TextureChecker":
+            m[L.M_TEX] = 1.0
+            m[L.M_TR:L.M_TB + 1] = (1.0, 1.0, 1.0)
+        elif hasattr(tex, "color"):
+            m[L.M_TEX] = 0.0
+            m[L.M_TR:L.M_TB + 1] = _xyz(tex.color)
+        else:
+            raise TypeError(f"unsupported texture {type(tex).__name__}")
+        # _calculate_physical_specular constants (shader.py:290-301), same Python expressions
+        alpha = sh.specular_roughness**2
+        F0 = ((sh.specular_ior - 1) / (sh.specular_ior + 1)) ** 2
+        m[L.M_A2] = alpha**2
+        m[L.M_A2M1] = alpha**2 - 1
+        m[L.M_1MA2] = 1 - alpha**2
+        m[L.M_F0] = F0
+        m[L.M_1MF0] = 1 - F0
+        # _calculate_physical_iridescence constants (shader.py:208-232)
+        hue_shift = (sh.thin_film_ior - 1.0) / 2.0
+        m[L.M_IG] = sh.iridescence_gain
+        m[L.M_TFW] = sh.thin_film_weight
+        m[L.M_TFT] = sh.thin_film_thickness
+        m[L.M_HS] = hue_shift
+        m[L.M_1MHS] = 1.0 - hue_shift
+        m[L.M_ROUGH] = sh.specular_roughness
+        m[L.M_REFL] = sh.reflection_gain
+        m[L.M_IOR] = sh.specular_ior
+        m[L.M_TFIOR] = sh.thin_film_ior
+    return blob
+
+
+def sphere_geometry(center, radius) -> np.ndarray:
+    """One RTX_GEOM_WORDS record for rtx_sphere_intersect."""
+    cx, cy, cz = center
+    g = np.zeros(L.GEOM_WORDS, dtype=np.float64)
+    g[L.G_CX:L.G_CZ + 1] = (cx, cy, cz)
+    g[L.G_CC] = (cx * cx + cy * cy) + cz * cz
+    g[L.G_RR] = radius * radius
+    g[L.G_INVR] = 1.0 / radius
+    return g
+
+
+def blob_key(blob: np.ndarray) -> bytes:
+    return hashlib.blake2b(blob.tobytes(), digest_size=16).digest()

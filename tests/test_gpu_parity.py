@@ -1,0 +1,177 @@
+"""GPU parity: the HIP path (C ABI via HipRenderer) against the reference fixtures and the CPU oracle.
+
+Tolerances. Geometry, the hit / shadow / checker decisions and the bounce structure are float64 with
+the reference's operation order and no contraction, so they match exactly; the only non-correctly-
+rounded operations are sin (iridescence) and pow (x^5, x^2.5 in the specular), where NumPy's SIMD
+versions and the device's differ by ~1 ulp. Hence colour is compared at max-abs <= 1e-12 (float64
+output; the largest unclipped values are ~1e2), uint8 output must be identical, and per-level ray
+counts must equal the oracle's.
+"""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import numpy_oracle as O
+from python_ray_tracer_amd import scenes
+from tests.conftest import GOLDEN, golden_png
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def hip():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from python_ray_tracer_amd.infrastructure import hip as H
+
+    return H
+
+
+def _render(H, spec, B, dtype=torch.float64, stats=False):
+    r = H.HipRenderer(max_bounces=B, color_dtype=dtype, collect_stats=stats)
+    scene = scenes.build_scene(spec)
+    col = r.raytrace_scene(scene.camera.position, r.get_ray_directions(scene.camera), scene)
+    return r, col.data.cpu().numpy()
+
+
+def test_golden_cases(hip, golden_meta, golden_renders):
+    for name, case in golden_meta["cases"].items():
+        _, got = _render(hip, case["spec"], case["max_bounces"])
+        ref = golden_renders[name]
+        err = np.abs(got - ref).max()
+        assert err <= ATOL, (name, err)
+        W, H = case["spec"]["camera"]["width"], case["spec"]["camera"]["height"]
+        assert np.array_equal(O.to_uint8(got, W, H), O.to_uint8(ref, W, H)), name
+
+
+def test_render_png_byte_exact(hip, tmp_path):
+    """main.py's scene with the reference's unbounded bounces -> the committed render.png."""
+    r = hip.HipRenderer()  # max_bounces=None, like the reference
+    scene = scenes.build_scene(scenes.main_spec(960, 540))
+    from python_ray_tracer_amd.application import render_image_pipeline
+
+    out = tmp_path / "render.png"
+    render_image_pipeline(scene, out, r)
+    from PIL import Image
+
+    assert np.array_equal(np.asarray(Image.open(out).convert("RGB")), golden_png("render_main_960x540.png"))
+
+
+@pytest.mark.parametrize("tag", ["main", "readme"])
+def test_1080p_B3_full_size(hip, golden_meta, tag):
+    """BASELINE configs[1] size: 1920x1080, 3 bounces, against the oracle at full size and the
+    reference's own uint8 output; kernel ray counters against the oracle's."""
+    m = golden_meta[f"ref_1080p_B3_{tag}"]
+    r, got = _render(hip, m["spec"], 3, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(m["spec"]), 3, stats=st)
+    assert np.abs(got - want).max() <= ATOL
+    assert np.array_equal(O.to_uint8(got, 1920, 1080), golden_png(f"ref_1080p_B3_{tag}.png"))
+    s = r.stats()
+    assert s["rays"] == st.rays and s["hits"] == st.hits
+    assert s["pixels"] == 1920 * 1080 and s["deferred"] == 0
+    # float32 output = float64 output rounded once
+    _, got32 = _render(hip, m["spec"], 3, dtype=torch.float32)
+    assert np.array_equal(got32, got.astype(np.float32))
+
+
+def test_ties_take_the_general_kernel(hip, golden_meta, golden_renders):
+    case = golden_meta["cases"]["ties_64x36_B2"]
+    r, got = _render(hip, case["spec"], 2, stats=True)
+    assert np.abs(got - golden_renders["ties_64x36_B2"]).max() <= ATOL
+    s = r.stats()
+    assert s["deferred"] > 100 and s["ties"] >= s["deferred"]
+
+
+@pytest.mark.parametrize("B", [0, 1, 2, 4, 5, 6, 7, 8, 9, 12])
+def test_every_bounce_cap(hip, B):
+    spec = scenes.random_spec(16, 0, 128, 72)
+    _, got = _render(hip, spec, B)
+    want = O.render(O.scene_from_spec(spec), B)
+    assert np.abs(got - want).max() <= ATOL, B
+
+
+def test_c3_c4_scenes_reduced_size(hip):
+    for spec, B in ((scenes.random_spec(16, 0, 480, 270), 4), (scenes.random_spec(64, 0, 320, 180), 5),
+                    (scenes.with_camera(scenes.random_spec(16, 0, 320, 180), scenes.orbit_position(100)), 3)):
+        r, got = _render(hip, spec, B, stats=True)
+        st = O.TraceStats()
+        want = O.render(O.scene_from_spec(spec), B, stats=st)
+        assert np.abs(got - want).max() <= ATOL
+        assert r.stats()["rays"] == st.rays
+
+
+def test_row_tiles_reassemble(hip):
+    from python_ray_tracer_amd import tiling
+
+    spec = scenes.readme_spec(200, 117)
+    scene = scenes.build_scene(spec)
+    r = hip.HipRenderer(max_bounces=3)
+    full = r.render(scene).data
+    for P, rb in ((2, 8), (3, 5), (8, 8)):
+        tiles = [r.render_tile(scene, rb, P, p) for p in range(P)]
+        rmax = tiling.max_local_rows(117, rb, P)
+        padded = [torch.nn.functional.pad(t, (0, rmax * 200 - t.shape[1])) for t in tiles]
+        assert torch.equal(tiling.assemble(padded, 117, 200, rb), full)
+        u8 = [r.render_tile(scene, rb, P, p, out="u8") for p in range(P)]
+        u8 = [torch.nn.functional.pad(t, (0, 0, 0, 0, 0, rmax - t.shape[0])) for t in u8]
+        assert torch.equal(tiling.assemble(u8, 117, 200, rb, layout="hwc"), r.quantize(r.render(scene), scene.camera))
+
+
+def test_explicit_rays_and_intersect(hip, golden_meta):
+    """rtx_trace_rays (raytrace_scene on arbitrary rays) and rtx_sphere_intersect (shape.py:28-51)."""
+    spec = scenes.readme_spec(64, 36)
+    sc = O.scene_from_spec(spec)
+    r = hip.HipRenderer(max_bounces=3)
+    scene = scenes.build_scene(spec)
+    d = O.ray_directions(sc.cam, 64, 36)
+    # materialised get_ray_directions equals the oracle bit for bit
+    dirs = r.get_ray_directions(scene.camera)
+    assert np.array_equal(dirs.data.cpu().numpy(), np.stack(d))
+    # explicit rays with a shared origin == the fused camera path
+    got = r.raytrace_scene(scene.camera.position, hip.HipVector3D(*d), scene).data.cpu().numpy()
+    assert np.abs(got - O.render(sc, 3)).max() <= ATOL
+    # per-ray origins (a second-level batch: offset origins)
+    rng = np.random.default_rng(1)
+    o = [np.full(d[0].shape, v) + rng.uniform(-0.1, 0.1, d[0].shape) for v in sc.cam]
+    got = r.raytrace_scene(hip.HipVector3D(*o), hip.HipVector3D(*d), scene).data.cpu().numpy()
+    want = np.stack(O.trace(sc, tuple(o), d, 3))
+    assert np.abs(got - want).max() <= ATOL
+    # intersect known answers
+    for k in json.loads((GOLDEN / "intersect_kat.json").read_text()):
+        s = hip.HipSphere(hip.HipVector3D(*k["center"]), k["radius"], None)
+        t = s.intersect(hip.HipVector3D(*k["origin"]), hip.HipVector3D(*[np.array([v]) for v in k["dir"]]))
+        assert float(t[0]) == k["t"], k["label"]
+
+
+def test_quantize_matches_numpy(hip):
+    r = hip.HipRenderer(max_bounces=1)
+    vals = np.concatenate([np.linspace(-0.5, 1.5, 4001), [0, 1, 1 / 255, 2 / 255, 254.99999 / 255, np.inf, -np.inf]])
+    n = vals.size
+    c = np.stack([vals, vals[::-1], np.roll(vals, 7)])
+    from python_ray_tracer_amd.domain import Camera
+
+    cam = Camera(hip.HipVector3D(0, 0, -1), n, 1)
+    got = r.quantize(hip.HipRGBColor.from_tensor(torch.from_numpy(c).cuda()), cam).cpu().numpy()
+    assert np.array_equal(got, O.to_uint8(c, n, 1))
+
+
+def test_unbounded_recursion_limit(hip):
+    """Rays trapped inside a mirror sphere reflect forever (a negative radius flips the normal, so
+    the nudged point stays inside): the reference hits Python's recursion limit; HipRenderer raises
+    RecursionError past UNBOUNDED_LEVELS."""
+    spec = scenes.readme_spec(8, 8)
+    spec["spheres"] = [{"center": [0, 0.2, -2], "radius": -5.0,
+                        "shader": {"reflection_gain": 1, "specular_gain": 1.0, "specular_roughness": 0.5,
+                                   "iridescence_gain": 0, "diffuse_gain": 0.5,
+                                   "texture": {"kind": "const", "color": [1, 1, 1]}}}]
+    spec["lights"][0]["position"] = [0, 0.2, -2]
+    r = hip.HipRenderer()
+    scene = scenes.build_scene(spec)
+    with pytest.raises(RecursionError):
+        r.render(scene)

@@ -1,0 +1,151 @@
+"""CPU-only tests of the host layer: C-ABI library exports, scene packing, tiling, error behaviour.
+No compute call reaches the GPU here."""
+
+import ctypes
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import numpy_oracle as O
+from python_ray_tracer_amd import scenes, tiling
+from python_ray_tracer_amd.infrastructure.hip import _lib as L
+from python_ray_tracer_amd.infrastructure.hip import scene_pack
+from tests.conftest import REPO
+
+
+def _header_functions():
+    text = (REPO / "include" / "rtx_hip.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(rtx_\w+)\(", text, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = L.load()
+    declared = _header_functions()
+    assert set(declared) == set(L.EXPORTS), declared
+    for name in declared:
+        assert hasattr(lib, name), name
+        assert ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
+
+
+def test_abi_layout_matches_header():
+    text = (REPO / "include" / "rtx_hip.h").read_text()
+
+    def const(name):
+        m = re.search(rf"\b{name}\s*=\s*(-?\d+)", text) or re.search(rf"#define\s+{name}\s+\(?(-?[\d.]+)", text)
+        return float(m.group(1))
+
+    assert const("RTX_HDR_WORDS") == L.HDR_WORDS
+    assert const("RTX_GEOM_WORDS") == L.GEOM_WORDS
+    assert const("RTX_MAT_WORDS") == L.MAT_WORDS
+    assert const("RTX_S_WORDS") == L.S_WORDS
+    assert const("RTX_H_CAMOO") == L.H_CAMOO
+    assert const("RTX_M_TFIOR") == L.M_TFIOR
+    assert const("RTX_G_C0") == L.G_C0
+    assert const("RTX_MAGIC") == L.MAGIC
+    assert const("RTX_UNBOUNDED_LEVELS") == L.UNBOUNDED_LEVELS
+    lay = (ctypes.c_int * 8)()
+    assert L.load().rtx_abi_version(lay, 8) == L.ABI_VERSION
+
+
+def test_workspace_bytes_and_error_paths():
+    lib = L.load()
+    assert lib.rtx_workspace_bytes(1920 * 1080, 3) >= L.WS_HDR_BYTES + 8 * 1920 * 1080
+    # argument validation happens before any HIP call: no GPU needed
+    rc = lib.rtx_render_camera(None, 3, 16, 16, 1, 1, 0, 16, 3, None, 0, None, 0, None, None)
+    assert rc == -1 and b"null" in lib.rtx_last_error()
+    rc = lib.rtx_render_camera(None, 3, 16, 16, 1, 2, 5, 16, 3, None, 0, None, 0, None, None)
+    assert rc == -1 and b"geometry" in lib.rtx_last_error()
+    assert lib.rtx_quantize_u8(None, 0, 10, None, None) == -1
+    assert lib.rtx_sphere_intersect(None, None, 0, None, 5, None, None) == -1
+
+
+def test_pack_matches_reference_expressions():
+    spec = scenes.readme_spec(160, 90)
+    sc = scenes.build_scene(spec)  # HipSphere & co. need no GPU to construct
+    blob = scene_pack.pack_scene(sc)
+    S = len(spec["spheres"])
+    assert blob[L.H_NSPH] == S and blob[L.H_MAGIC] == L.MAGIC
+    geo = blob[L.HDR_WORDS:L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, -1)
+    mat = blob[L.HDR_WORDS + S * L.GEOM_WORDS:].reshape(S, -1)
+    # level-0 "c" of shape.py:35-37 equals the oracle's scalar evaluation
+    for s, sp in enumerate(spec["spheres"]):
+        cx, cy, cz = sp["center"]
+        ox, oy, oz = spec["camera"]["position"]
+        c = ((cx * cx + cy * cy) + cz * cz) + ((ox * ox + oy * oy) + oz * oz) - 2 * ((cx * ox + cy * oy) + cz * oz) \
+            - (sp["radius"] * sp["radius"])
+        assert geo[s, L.G_C0] == c
+        assert geo[s, L.G_INVR] == 1.0 / sp["radius"]
+        r = sp["shader"]["specular_roughness"]
+        assert mat[s, L.M_A2] == (r**2) ** 2
+        assert mat[s, L.M_F0] == ((1.5 - 1) / (1.5 + 1)) ** 2
+    assert mat[2, L.M_TEX] == 1.0 and mat[0, L.M_TEX] == 0.0
+    # linspace parameters reproduce np.linspace exactly
+    for W, H in ((1, 1), (2, 3), (7, 5), (960, 540), (1920, 1080), (7680, 4320)):
+        cw = scene_pack.camera_words((0.0, 0.2, -2.0), W, H)
+        ar = float(W) / H
+        for (start, step, stop, fix), want in ((cw["xs"], np.linspace(-1, 1, W)),
+                                               (cw["ys"], np.linspace(1 / ar + 0.25, -1 / ar + 0.25, H))):
+            i = np.arange(len(want), dtype=np.float64)
+            got = i * step + start
+            if fix:
+                got[-1] = stop
+            assert np.array_equal(got, want), (W, H)
+
+
+def test_pack_error_behaviour():
+    from python_ray_tracer_amd.domain import Camera, DomeLight, Scene3D
+    from python_ray_tracer_amd.infrastructure.hip import HipRGBColor, HipVector3D
+
+    spec = scenes.readme_spec(8, 8)
+    sc = scenes.build_scene(spec)
+    with pytest.raises(TypeError):  # reduce() of empty iterable (base.py:98)
+        scene_pack.pack_scene(Scene3D([], sc.lights, sc.camera))
+    with pytest.raises(IndexError):  # scene.lights[0] (shader.py:75)
+        scene_pack.pack_scene(Scene3D(sc.shapes, [], sc.camera))
+    with pytest.raises(AttributeError):  # DomeLight has no position (shader.py:75)
+        scene_pack.pack_scene(Scene3D(sc.shapes, [DomeLight(0.1, HipRGBColor(1, 1, 1))], sc.camera))
+    with pytest.raises(ValueError):
+        scene_pack.pack_scene(Scene3D(sc.shapes, sc.lights, Camera(HipVector3D(0, 0, -2), 0, 5)))
+
+
+@pytest.mark.parametrize("H,rb,P", [(1080, 8, 8), (1080, 8, 3), (13, 4, 3), (5, 8, 2), (4320, 8, 8), (7, 1, 7)])
+def test_tiling_partition(H, rb, P):
+    seen = np.concatenate([tiling.tile_rows(H, rb, P, p) for p in range(P)])
+    assert np.array_equal(np.sort(seen), np.arange(H))
+    for p in range(P):
+        r = tiling.tile_rows(H, rb, P, p)
+        assert len(r) == tiling.n_local_rows(H, rb, P, p)
+        assert np.all(np.diff(r) > 0)
+    # assemble inverts the split
+    W = 3
+    frame = np.arange(3 * H * W, dtype=np.float64).reshape(3, H, W)
+    rmax = tiling.max_local_rows(H, rb, P)
+    tiles = []
+    for p in range(P):
+        r = tiling.tile_rows(H, rb, P, p)
+        t = np.zeros((3, rmax, W))
+        t[:, :len(r)] = frame[:, r]
+        tiles.append(torch.from_numpy(t.reshape(3, rmax * W)))
+    full = tiling.assemble(tiles, H, W, rb).numpy()
+    assert np.array_equal(full, frame.reshape(3, H * W))
+
+
+def test_hip_renderer_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        HipRenderer()
+
+
+def test_random_scene_generator_is_seeded():
+    a = scenes.random_spec(16, 0)
+    b = scenes.random_spec(16, 0)
+    assert a == b and len(a["spheres"]) == 17
+    for s in a["spheres"][:-1]:
+        assert abs(s["center"][1] - (s["radius"] - 0.5)) < 1e-15
+    sc = O.scene_from_spec(a)
+    assert sc.spheres[-1].checker and sc.light_pos == (-2, 4, -1)
