@@ -133,10 +133,13 @@ enum {
   RTX_S_WORDS = 136
 };
 
-/* workspace: status words then deferred-ray list then per-worker frame stacks */
+/* workspace: status words then deferred-ray list then per-worker frame stacks.
+ * The workspace must be zero-filled before its first use; every call leaves the counters zeroed
+ * again (no per-call memset). RTX_WS_STATUS flags are sticky: the caller reads and clears them. */
 enum {
   RTX_WS_COUNT = 0,    /* uint32: deferred rays            */
   RTX_WS_STATUS = 1,   /* uint32: RTX_ST_* flags           */
+  RTX_WS_DONE = 2,     /* uint32: finished blocks of the general kernel (reset by the last one) */
   RTX_WS_HDR_BYTES = 256
 };
 enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2 };

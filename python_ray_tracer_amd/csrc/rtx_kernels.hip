@@ -8,18 +8,25 @@
 // -ffp-contract=off because NumPy never fuses a multiply into an add.
 //
 // Kernels
-//   k_render_fast<B>  B <= RTX_FAST_MAX_BOUNCES. The reference's recursion
+//   k_render_fast<B, LDS>  B <= RTX_FAST_MAX_BOUNCES. The reference's recursion
 //                     raytrace_scene -> create -> _calculate_reflection -> raytrace_scene
 //                     (base.py:91-121, shader.py:63-161) becomes an in-register loop over bounce
-//                     levels. The per-level shading terms (A, spec, g, irid) of the non-terminal
-//                     levels sit in a compile-time-sized shift register and are folded back from
-//                     the deepest level, reproducing the reference association
+//                     levels. For every non-terminal level a compile-time-sized shift register keeps
+//                     the INPUTS of that level's colour terms (max(N.L,0), the dome sum, the specular,
+//                     N.V, the hit sphere and its checker bit: 4 doubles + 1 int); the fold from the
+//                     deepest level recomputes A and I from them with the same instructions and
+//                     applies the reference association
 //                         col_k = ((A_k + (spec_k + col_{k+1}*0.5)*g_k) + I_k)      (shader.py:106-110)
-//                     exactly. A ray that meets a tie (two shapes at the same nearest distance,
-//                     base.py:103 — both get shaded and summed) is appended to a deferred list.
+//                     exactly. Sphere geometry is read by the wave-uniform loops through the scalar
+//                     cache (s_load); the per-lane hit-sphere/material records come from an LDS copy
+//                     of the scene table (LDS = S <= kLdsMaxSpheres). A ray that meets a tie (two
+//                     shapes at the same nearest distance, base.py:103 — both get shaded and summed)
+//                     is appended to a deferred list.
 //   k_render_general  Any bounce cap, ties included: an explicit depth-first walk of the ray tree
 //                     with per-worker frame stacks in the workspace (HBM). Serves the deferred
-//                     list of k_render_fast, and every ray when B > RTX_FAST_MAX_BOUNCES.
+//                     list of k_render_fast, and every ray when B > RTX_FAST_MAX_BOUNCES. Its last
+//                     block resets the list counter, so the workspace is left zeroed for the next
+//                     call (no per-frame memset).
 //   k_ray_dirs, k_intersect, k_quantize — the remaining boundary functions.
 #include <hip/hip_runtime.h>
 
@@ -38,6 +45,13 @@ constexpr int kBlock = 256;   // 4 waves
 constexpr int kTileW = 16;    // block tile: 16 x 16 pixels, each wave an 8 x 8 sub-tile
 constexpr int kTileH = 16;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
+constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
+constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
+constexpr int kDeferredWorkers = 4096;  // general-kernel threads when it only serves ties
+
+// Wave-uniform loads through the scalar cache: the constant address space makes hipcc emit s_load
+// even though the kernel also stores (it cannot prove the scene blob is not aliased otherwise).
+typedef const double __attribute__((address_space(4))) cdouble;
 
 struct Params {
   const double* scene;
@@ -99,8 +113,9 @@ __device__ __forceinline__ int trunc_parity(double x) {
 
 // NumpySphere.intersect, shape.py:28-51, for a ray with precomputed oo = O.O.
 // b = 2 * D.(O - C);  c = ((C.C + O.O) - 2 * C.O) - r*r;  disc = b^2 - 4c.
-__device__ __forceinline__ double isect(const double* __restrict__ g, double ox, double oy, double oz, double oo,
-                                        double dx, double dy, double dz) {
+template <typename P>
+__device__ __forceinline__ double isect(const P* g, double ox, double oy, double oz, double oo, double dx, double dy,
+                                        double dz) {
   const double cx = g[RTX_G_CX], cy = g[RTX_G_CY], cz = g[RTX_G_CZ];
   const double b = 2.0 * dot3(dx, dy, dz, ox - cx, oy - cy, oz - cz);
   const double c = ((g[RTX_G_CC] + oo) - 2.0 * dot3(cx, cy, cz, ox, oy, oz)) - g[RTX_G_RR];
@@ -116,9 +131,10 @@ __device__ __forceinline__ double isect(const double* __restrict__ g, double ox,
   return t;
 }
 
-// Same, level-0 camera origin: O - C and c precomputed on the host with the same expressions.
-__device__ __forceinline__ double isect_cam(const double* __restrict__ g, double ocx, double ocy, double ocz,
-                                            double dx, double dy, double dz) {
+// Same, level-0 camera origin: O - C and c precomputed with the same expressions (host: c, here
+// O - C from uniform values).
+__device__ __forceinline__ double isect_cam(const cdouble* g, double ocx, double ocy, double ocz, double dx, double dy,
+                                            double dz) {
   const double b = 2.0 * dot3(dx, dy, dz, ocx, ocy, ocz);
   const double disc = (b * b) - (4.0 * g[RTX_G_C0]);
   double t = FARAWAY;
@@ -140,106 +156,78 @@ __device__ __forceinline__ double pow5(double x) {
 }
 __device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt(x); }
 
-struct Shade {
-  double ar, ag, ab;  // ((0.004 + diffuse) + dome)           shader.py:86-98
-  double spec;        // physical specular (0 unless lit && g != 0: multiplied away otherwise)
-  double g;           // specular_gain
-  bool lit;           // shadow test                          shader.py:79-84
-  double ir, ig, ib;  // iridescence                          shader.py:110
-  double qx, qy, qz;  // nudged hit point (child ray origin)  shader.py:77
+// The inputs of one shaded hit's colour terms (everything else comes from the material record).
+struct Hit {
+  double dli;    // max(N.L, 0)                                shader.py:138
+  double di;     // sum_domes intensity * max(N.(0,1,0), 0)     shader.py:239-242
+  double spec;   // physical specular (0 unless lit && g != 0)  shader.py:100-104
+  double va;     // clip(N.V, 0, 1) (iridescence input)         shader.py:201
+  double g;      // specular_gain
+  int h;         // hit sphere
+  bool chk;      // checker cell                                 shader.py:30
+  bool lit;      //                                              shader.py:79-84
+  double qx, qy, qz;  // nudged hit point = reflected ray origin  shader.py:77
   double nx, ny, nz;  // normal
 };
 
-// NumpyShader.create (shader.py:63-112) for one hit of sphere `h` at distance t, minus the
-// reflection recursion, which the caller drives. Returns with the normal in s.n*.
-__device__ __forceinline__ void shade_hit(const double* __restrict__ sc, const double* __restrict__ geo,
-                                          const double* __restrict__ mat, int nsph, int h, double ox, double oy,
-                                          double oz, double dx, double dy, double dz, double t, Shade& s) {
-  const double* gh = geo + h * RTX_GEOM_WORDS;
-  const double* mh = mat + h * RTX_MAT_WORDS;
-  const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73
-  const double inv_r = gh[RTX_G_INVR];
-  const double nx = (px - gh[RTX_G_CX]) * inv_r;  // :74 (not renormalised)
-  const double ny = (py - gh[RTX_G_CY]) * inv_r;
-  const double nz = (pz - gh[RTX_G_CZ]) * inv_r;
-  double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
-  norm3(lx, ly, lz);  // :75
-  double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
-  norm3(vx, vy, vz);  // :76 (towards the camera on every level)
-  const double qx = px + nx * 0.0001, qy = py + ny * 0.0001, qz = pz + nz * 0.0001;  // :77
+// _calculate_physical_specular, shader.py:246-320, for unit-ish L (once normalised) and V.
+template <typename M>
+__device__ __forceinline__ double specular(const M* mh, double g, double nx, double ny, double nz, double lx,
+                                           double ly, double lz, double vx, double vy, double vz) {
+  double Lx = lx, Ly = ly, Lz = lz;
+  norm3(Lx, Ly, Lz);  // :278 (normalised a second time)
+  double Vx = vx, Vy = vy, Vz = vz;
+  norm3(Vx, Vy, Vz);  // :279
+  double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
+  norm3(Hx, Hy, Hz);  // :280
+  const double NdotV = clip01(dot3(nx, ny, nz, Vx, Vy, Vz));  // :283
+  const double NdotH = clip01(dot3(nx, ny, nz, Hx, Hy, Hz));  // :284
+  const double VdotH = clip01(dot3(Vx, Vy, Vz, Hx, Hy, Hz));  // :285
+  const double NdotL = clip01(dot3(nx, ny, nz, Lx, Ly, Lz));  // :287
+  const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
+  const double a2 = mh[RTX_M_A2];
+  const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
+  const double D = a2 / (RTX_PI * ((denom * denom) + 1e-8));  // :296
+  const double oma2 = mh[RTX_M_1MA2];
+  const double G1L = (2.0 * NdotL) / ((NdotL + sqrt(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
+  const double G1V = (2.0 * NdotV) / ((NdotV + sqrt(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
+  const double G = G1L * G1V;  // :303
+  const double spec_base = ((F * D) * G) / ((4.0 * NdotV) + 1e-8);  // :306
+  const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
+  const double sf = spec_base + g * glint;  // :315
+  return (NdotV <= 0.0) ? 0.0 : sf;  // :318
+}
 
-  // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
-  // Equivalent any-hit form: lit unless some sphere is strictly nearer than the shape itself.
-  const double qq = dot3(qx, qy, qz, qx, qy, qz);
-  const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
-  bool lit = true;
-  for (int j = 0; j < nsph; ++j) {
-    if (isect(geo + j * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz) < tself) {
-      lit = false;
-      break;
-    }
-  }
+// Colour of one shaded hit given the reflected colour R (shader.py:86-110):
+//   ((((0.004 + diffuse) + dome) + (spec + R*0.5)*g*lit) + irid)
+// `weighted` = lit && g != 0; otherwise the specular/reflection term is x*0 == 0 (R is finite).
+template <typename M>
+__device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double dli, double di, bool chk, bool lit,
+                                          bool weighted, double spec, double va, double Rr, double Rg, double Rb,
+                                          double& cr, double& cg, double& cb) {
   const double litf = lit ? 1.0 : 0.0;
-
-  // ambient + diffuse (:86-88, :130-141): 0.004 + ((tex * max(N.L, 0)) * lit) * diffuse_gain
-  const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));
   double tr, tg, tb;
-  if (mh[RTX_M_TEX] != 0.0) {  // TextureChecker.get_color (:29-32)
-    const double c = (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0)) ? 1.0 : 0.0;
-    tr = tg = tb = c;
+  if (mh[RTX_M_TEX] != 0.0) {  // TextureChecker.get_color (:29-32): white * checker
+    tr = tg = tb = chk ? 1.0 : 0.0;
   } else {  // Texture.get_color (:17-19)
     tr = mh[RTX_M_TR];
     tg = mh[RTX_M_TG];
     tb = mh[RTX_M_TB];
   }
   const double dg = mh[RTX_M_DG];
-  double ar = 0.004 + ((tr * dli) * litf) * dg;
-  double ag = 0.004 + ((tg * dli) * litf) * dg;
-  double ab = 0.004 + ((tb * dli) * litf) * dg;
-
-  // dome light (:234-244): sum_i intensity_i * max(N.(0,1,0), 0), times the last dome colour
-  const double up = ((nx * 0.0) + (ny * 1.0)) + (nz * 0.0);
-  const int ndome = (int)sc[RTX_H_NDOME];
-  double di = 0.0;
-  for (int j = 0; j < ndome; ++j) di = di + sc[RTX_H_DOMEI + j] * max0(up);
-  ar = ar + sc[RTX_H_DOMEC + 0] * di;
-  ag = ag + sc[RTX_H_DOMEC + 1] * di;
-  ab = ab + sc[RTX_H_DOMEC + 2] * di;
-
-  // physical specular (:246-320). Only observable through (spec + 0.5 R) * g * lit (:106), so
-  // it is skipped when g == 0 or in shadow (finite * 0 == 0).
+  // ambient + diffuse (:86-88, :138-141), dome (:98, :244)
+  const double ar = (0.004 + ((tr * dli) * litf) * dg) + sc[RTX_H_DOMEC + 0] * di;
+  const double ag = (0.004 + ((tg * dli) * litf) * dg) + sc[RTX_H_DOMEC + 1] * di;
+  const double ab = (0.004 + ((tb * dli) * litf) * dg) + sc[RTX_H_DOMEC + 2] * di;
+  // specular + reflection (:106)
   const double g = mh[RTX_M_G];
-  double spec = 0.0;
-  if (lit && g != 0.0) {
-    double Lx = lx, Ly = ly, Lz = lz;
-    norm3(Lx, Ly, Lz);  // :278 (normalised a second time)
-    double Vx = vx, Vy = vy, Vz = vz;
-    norm3(Vx, Vy, Vz);  // :279
-    double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
-    norm3(Hx, Hy, Hz);  // :280
-    const double NdotV = clip01(dot3(nx, ny, nz, Vx, Vy, Vz));  // :283
-    const double NdotH = clip01(dot3(nx, ny, nz, Hx, Hy, Hz));  // :284
-    const double VdotH = clip01(dot3(Vx, Vy, Vz, Hx, Hy, Hz));  // :285
-    const double NdotL = clip01(dot3(nx, ny, nz, Lx, Ly, Lz));  // :287
-    const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
-    const double a2 = mh[RTX_M_A2];
-    const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
-    const double D = a2 / (RTX_PI * ((denom * denom) + 1e-8));  // :296
-    const double oma2 = mh[RTX_M_1MA2];
-    const double G1L = (2.0 * NdotL) / ((NdotL + sqrt(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
-    const double G1V = (2.0 * NdotV) / ((NdotV + sqrt(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
-    const double G = G1L * G1V;  // :303
-    const double spec_base = ((F * D) * G) / ((4.0 * NdotV) + 1e-8);  // :306
-    const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
-    const double sf = spec_base + g * glint;  // :315
-    spec = (NdotV <= 0.0) ? 0.0 : sf;  // :318
-  }
-
-  // thin-film iridescence (:186-232); skipped when iridescence_gain == 0 (x * 0 == 0)
+  const double xr = weighted ? (spec + Rr * 0.5) * g : 0.0;
+  const double xg = weighted ? (spec + Rg * 0.5) * g : 0.0;
+  const double xb = weighted ? (spec + Rb * 0.5) * g : 0.0;
+  // thin-film iridescence (:186-232); zero when iridescence_gain == 0 (x * 0 == 0)
   double ir = 0.0, ig = 0.0, ib = 0.0;
   const double igain = mh[RTX_M_IG];
   if (igain != 0.0) {
-    const double va = clip01(dot3(nx, ny, nz, vx, vy, vz));  // :201
     const double af = fabs(va - 0.5) * 2.0;  // :204
     const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
     const double ip = sin(phase);  // :211
@@ -252,11 +240,67 @@ __device__ __forceinline__ void shade_hit(const double* __restrict__ sc, const d
     ig = (gg * w) * igain;
     ib = (b * w) * igain;
   }
-  s.ar = ar; s.ag = ag; s.ab = ab;
+  cr = (ar + xr) + ir;
+  cg = (ag + xg) + ig;
+  cb = (ab + xb) + ib;
+}
+
+// NumpyShader.create (shader.py:63-112) for a hit of sphere h at distance t, minus the colour
+// assembly (hit_color) and the reflection recursion (driven by the caller).
+// geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
+// same table (LDS copy or global).
+template <typename T>
+__device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, const T* tab, int nsph, int h, double ox,
+                                      double oy, double oz, double dx, double dy, double dz, double t, Hit& s) {
+  const T* gh = tab + h * RTX_GEOM_WORDS;
+  const T* mh = tab + nsph * RTX_GEOM_WORDS + h * RTX_MAT_WORDS;
+  const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73
+  const double inv_r = gh[RTX_G_INVR];
+  const double nx = (px - gh[RTX_G_CX]) * inv_r;  // :74 (not renormalised)
+  const double ny = (py - gh[RTX_G_CY]) * inv_r;
+  const double nz = (pz - gh[RTX_G_CZ]) * inv_r;
+  double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
+  norm3(lx, ly, lz);  // :75
+  const double qx = px + nx * 0.0001, qy = py + ny * 0.0001, qz = pz + nz * 0.0001;  // :77
+
+  // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
+  // Equivalent any-hit form: lit unless some sphere is strictly nearer than the shape itself.
+  const double qq = dot3(qx, qy, qz, qx, qy, qz);
+  const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
+  bool lit = true;
+  for (int j = 0; j < nsph; ++j) {
+    const int ju = __builtin_amdgcn_readfirstlane(j);
+    if (isect(geo + ju * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz) < tself) {
+      lit = false;
+      break;
+    }
+  }
+
+  const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));  // :138
+  // dome (:239-242): light_direction (0, 1, 0)
+  const double up = ((nx * 0.0) + (ny * 1.0)) + (nz * 0.0);
+  const int ndome = (int)sc[RTX_H_NDOME];
+  double di = 0.0;
+  for (int j = 0; j < ndome; ++j) di = di + sc[RTX_H_DOMEI + j] * max0(up);
+
+  const double g = mh[RTX_M_G];
+  const bool weighted = lit && g != 0.0;
+  const bool need_irid = mh[RTX_M_IG] != 0.0;
+  double spec = 0.0, va = 0.0;
+  if (weighted || need_irid) {
+    double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
+    norm3(vx, vy, vz);  // :76 (towards the camera on every level)
+    if (weighted) spec = specular(mh, g, nx, ny, nz, lx, ly, lz, vx, vy, vz);
+    if (need_irid) va = clip01(dot3(nx, ny, nz, vx, vy, vz));  // :201
+  }
+  s.dli = dli;
+  s.di = di;
   s.spec = spec;
+  s.va = va;
   s.g = g;
+  s.h = h;
+  s.chk = (mh[RTX_M_TEX] != 0.0) && (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0));  // :30
   s.lit = lit;
-  s.ir = ir; s.ig = ig; s.ib = ib;
   s.qx = qx; s.qy = qy; s.qz = qz;
   s.nx = nx; s.ny = ny; s.nz = nz;
 }
@@ -280,8 +324,8 @@ __device__ __forceinline__ int global_row(const Params& p, int lr) {
 }
 
 // get_ray_directions (base.py:123-141) for pixel (col, global row r).
-__device__ __forceinline__ void camera_dir(const double* __restrict__ sc, int col, int r, int W, int H, double& dx,
-                                           double& dy, double& dz) {
+__device__ __forceinline__ void camera_dir(const cdouble* sc, int col, int r, int W, int H, double& dx, double& dy,
+                                           double& dz) {
   // np.linspace: i*step + start, last element set to stop exactly
   const double x = (sc[RTX_H_XFIX] != 0.0 && col == W - 1) ? sc[RTX_H_XSTOP]
                                                             : (double)col * sc[RTX_H_XSTEP] + sc[RTX_H_XSTART];
@@ -299,19 +343,20 @@ __device__ __forceinline__ void camera_dir(const double* __restrict__ sc, int co
 
 __device__ __forceinline__ void load_ray(const Params& p, int64_t i, double& ox, double& oy, double& oz, double& dx,
                                          double& dy, double& dz) {
+  const cdouble* sc = (const cdouble*)p.scene;
   if (p.mode == 0) {
     const int lr = (int)(i / p.width), col = (int)(i % p.width);
-    camera_dir(p.scene, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
-    ox = p.scene[RTX_H_CAM + 0];
-    oy = p.scene[RTX_H_CAM + 1];
-    oz = p.scene[RTX_H_CAM + 2];
+    camera_dir(sc, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
+    ox = sc[RTX_H_CAM + 0];
+    oy = sc[RTX_H_CAM + 1];
+    oz = sc[RTX_H_CAM + 2];
   } else {
     const int64_t n = p.n;
     dx = p.dir[i];
     dy = p.dir[n + i];
     dz = p.dir[2 * n + i];
-    const int64_t j = p.org_stride ? i : 0;
     const int64_t s = p.org_stride;
+    const int64_t j = s ? i : 0;
     ox = p.org[j];
     oy = p.org[s + j + (s ? 0 : 1)];
     oz = p.org[2 * s + j + (s ? 0 : 2)];
@@ -319,9 +364,9 @@ __device__ __forceinline__ void load_ray(const Params& p, int64_t i, double& ox,
 }
 
 __device__ __forceinline__ unsigned char quant_u8(double c) {
-  // (255 * np.clip(c, 0, 1)).astype(np.uint8)  (base.py:147): truncation
+  // (255 * np.clip(c, 0, 1)).astype(np.uint8)  (base.py:147): truncation (NaN -> 0)
   const double v = 255.0 * clip01(c);
-  return (unsigned char)(int)v;
+  return v >= 0.0 ? (unsigned char)(int)v : (unsigned char)0;
 }
 
 __device__ __forceinline__ void write_out(const Params& p, int64_t i, double r, double g, double b) {
@@ -348,15 +393,21 @@ __device__ __forceinline__ void stat_add(unsigned long long* st, int word, unsig
 }
 
 // ------------------------------------------------------------------------------------------
-// k_render_fast<B>
+// k_render_fast<B, LDS>
 // ------------------------------------------------------------------------------------------
 
-template <int B>
+template <int B, bool LDS>
 __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
-  const double* __restrict__ sc = p.scene;
-  const double* __restrict__ geo = sc + RTX_HDR_WORDS;
-  const double* __restrict__ mat = geo + p.nsph * RTX_GEOM_WORDS;
+  const cdouble* sc = (const cdouble*)p.scene;
+  const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
+
+  extern __shared__ double lds_tab[];
+  if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block
+    const double* src = p.scene + RTX_HDR_WORDS;
+    for (int k = threadIdx.x; k < nsph * kSphWords; k += kBlock) lds_tab[k] = src[k];
+    __syncthreads();
+  }
 
   int64_t i;
   if (p.mode == 0) {
@@ -376,21 +427,23 @@ __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
   unsigned long long* st = p.stats;
   if (st) stat_add(st, RTX_S_PIXELS, 1);
 
+  // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level)
   constexpr int NS = B > 0 ? B : 1;
-  double sA[NS][3], sS[NS], sG[NS], sI[NS][3];
+  double sDli[NS], sDi[NS], sSpec[NS], sVa[NS];
+  int sKey[NS];  // hit sphere | checker bit << 16
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
   bool deferred = false;
 
   for (int k = 0;; ++k) {
     if (st && k < RTX_S_LEVELS) stat_add(st, RTX_S_RAYS + k, 1);
-    // nearest hit over all shapes (base.py:97-103)
+    // nearest hit over all shapes (base.py:97-103), wave-uniform loop, geometry via s_load
     double tmin = FARAWAY;
     int hit = -1;
     bool tie = false;
     if (k == 0 && cam0) {
       for (int s = 0; s < nsph; ++s) {
-        const double* gs = geo + s * RTX_GEOM_WORDS;
+        const cdouble* gs = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
         const double t = isect_cam(gs, ox - gs[RTX_G_CX], oy - gs[RTX_G_CY], oz - gs[RTX_G_CZ], dx, dy, dz);
         if (t < tmin) {
           tmin = t;
@@ -403,7 +456,8 @@ __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
     } else {
       const double oo = dot3(ox, oy, oz, ox, oy, oz);
       for (int s = 0; s < nsph; ++s) {
-        const double t = isect(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
+        const cdouble* gs = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+        const double t = isect(gs, ox, oy, oz, oo, dx, dy, dz);
         if (t < tmin) {
           tmin = t;
           hit = s;
@@ -423,27 +477,28 @@ __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
       break;
     }
     if (st && k < RTX_S_LEVELS) stat_add(st, RTX_S_HITS + k, 1);
-    Shade s;
-    shade_hit(sc, geo, mat, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+    Hit s;
+    if constexpr (LDS) {
+      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+    } else {
+      shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+    }
     const bool weighted = s.lit && s.g != 0.0;
     if (!weighted || k >= B) {
-      // terminal level: reflection is black (capped) or multiplied by zero
-      const double t_r = weighted ? (s.spec + 0.0) * s.g : 0.0;
-      cr = (s.ar + t_r) + s.ir;
-      cg = (s.ag + t_r) + s.ig;
-      cb = (s.ab + t_r) + s.ib;
+      // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
+      const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
+      hit_color(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.chk, s.lit, weighted, s.spec,
+                s.va, 0.0, 0.0, 0.0, cr, cg, cb);
       break;
     }
-    // push this level's terms; the reflected ray becomes the next level
+    // push this level's colour inputs; the reflected ray becomes the next level
 #pragma unroll
     for (int j = NS - 1; j > 0; --j) {
-      sA[j][0] = sA[j - 1][0]; sA[j][1] = sA[j - 1][1]; sA[j][2] = sA[j - 1][2];
-      sS[j] = sS[j - 1]; sG[j] = sG[j - 1];
-      sI[j][0] = sI[j - 1][0]; sI[j][1] = sI[j - 1][1]; sI[j][2] = sI[j - 1][2];
+      sDli[j] = sDli[j - 1]; sDi[j] = sDi[j - 1]; sSpec[j] = sSpec[j - 1]; sVa[j] = sVa[j - 1];
+      sKey[j] = sKey[j - 1];
     }
-    sA[0][0] = s.ar; sA[0][1] = s.ag; sA[0][2] = s.ab;
-    sS[0] = s.spec; sG[0] = s.g;
-    sI[0][0] = s.ir; sI[0][1] = s.ig; sI[0][2] = s.ib;
+    sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
+    sKey[0] = hit | (s.chk ? 0x10000 : 0);
     ++depth;
     reflect_dir(dx, dy, dz, s.nx, s.ny, s.nz);
     ox = s.qx;
@@ -462,16 +517,17 @@ __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
     if (st) stat_add(st, RTX_S_DEFERRED, 1);
     return;
   }
-  // fold back (shader.py:106-110): col_k = ((A_k + (spec_k + col_{k+1}*0.5) * g_k) + I_k)
+  // fold back (shader.py:106-110): col_k = ((A_k + (spec_k + col_{k+1}*0.5) * g_k) + I_k); the
+  // stored levels were lit with g != 0
+  const double* mtab = (LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS) + nsph * RTX_GEOM_WORDS;
   for (int d = 0; d < depth; ++d) {
-    cr = (sA[0][0] + (sS[0] + cr * 0.5) * sG[0]) + sI[0][0];
-    cg = (sA[0][1] + (sS[0] + cg * 0.5) * sG[0]) + sI[0][1];
-    cb = (sA[0][2] + (sS[0] + cb * 0.5) * sG[0]) + sI[0][2];
+    const int key = sKey[0];
+    hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true, sSpec[0],
+              sVa[0], cr, cg, cb, cr, cg, cb);
 #pragma unroll
     for (int j = 0; j < NS - 1; ++j) {
-      sA[j][0] = sA[j + 1][0]; sA[j][1] = sA[j + 1][1]; sA[j][2] = sA[j + 1][2];
-      sS[j] = sS[j + 1]; sG[j] = sG[j + 1];
-      sI[j][0] = sI[j + 1][0]; sI[j][1] = sI[j + 1][1]; sI[j][2] = sI[j + 1][2];
+      sDli[j] = sDli[j + 1]; sDi[j] = sDi[j + 1]; sSpec[j] = sSpec[j + 1]; sVa[j] = sVa[j + 1];
+      sKey[j] = sKey[j + 1];
     }
   }
   write_out(p, i, cr, cg, cb);
@@ -481,9 +537,12 @@ __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
 // k_render_general: explicit depth-first ray tree (ties and any bounce cap)
 // ------------------------------------------------------------------------------------------
 
-// frame fields
+// frame fields: the ray, its nearest distance, the next shape to examine (-1: new ray), the
+// running colour sum over its hits (base.py:100-119), and the pending hit whose reflection is
+// being traced (its colour inputs).
 enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_TMIN, F_NEXT, F_AR, F_AG, F_AB,
-       F_PAR, F_PAG, F_PAB, F_PS, F_PG, F_PIR, F_PIG, F_PIB };
+       F_DLI, F_DI, F_SPEC, F_VA, F_KEY };
+static_assert(F_KEY < kFrameWords, "frame layout");
 
 struct Stack {
   double* base;
@@ -494,9 +553,10 @@ struct Stack {
 
 __device__ void trace_general(const Params& p, const Stack& S, double ox0, double oy0, double oz0, double dx0,
                               double dy0, double dz0, double& cr, double& cg, double& cb) {
-  const double* __restrict__ sc = p.scene;
-  const double* __restrict__ geo = sc + RTX_HDR_WORDS;
-  const double* __restrict__ mat = geo + p.nsph * RTX_GEOM_WORDS;
+  const cdouble* sc = (const cdouble*)p.scene;
+  const cdouble* geo = sc + RTX_HDR_WORDS;
+  const double* tab = p.scene + RTX_HDR_WORDS;
+  const double* mtab = tab + p.nsph * RTX_GEOM_WORDS;
   const int nsph = p.nsph;
   const int B = p.max_bounces;  // < 0: unbounded (bounded by the stack depth)
   unsigned long long* st = p.stats;
@@ -516,7 +576,7 @@ __device__ void trace_general(const Params& p, const Stack& S, double ox0, doubl
       tmin = FARAWAY;
       int nh = 0;
       for (int s = 0; s < nsph; ++s) {
-        const double t = isect(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
+        const double t = isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
         if (t < tmin) {
           tmin = t;
           nh = 1;
@@ -535,7 +595,7 @@ __device__ void trace_general(const Params& p, const Stack& S, double ox0, doubl
     int h = nsph;
     if (tmin != FARAWAY) {
       for (int s = next; s < nsph; ++s) {
-        if (isect(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz) == tmin) {
+        if (isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz) == tmin) {
           h = s;
           break;
         }
@@ -548,19 +608,20 @@ __device__ void trace_general(const Params& p, const Stack& S, double ox0, doubl
         return;
       }
       --d;  // fold into the parent's pending hit (shader.py:106-110), then add (base.py:119)
-      const double pg = S.at(d, F_PG), ps = S.at(d, F_PS);
-      const double xr = (S.at(d, F_PAR) + (ps + rr * 0.5) * pg) + S.at(d, F_PIR);
-      const double xg = (S.at(d, F_PAG) + (ps + rg * 0.5) * pg) + S.at(d, F_PIG);
-      const double xb = (S.at(d, F_PAB) + (ps + rb * 0.5) * pg) + S.at(d, F_PIB);
+      const int key = (int)S.at(d, F_KEY);
+      const int ph = key & 0xFFFF;
+      double xr, xg, xb;
+      hit_color(mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI), (key >> 16) != 0, true, true,
+                S.at(d, F_SPEC), S.at(d, F_VA), rr, rg, rb, xr, xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
       S.at(d, F_AB) = S.at(d, F_AB) + xb;
-      S.at(d, F_NEXT) = S.at(d, F_NEXT) + 1.0;
+      S.at(d, F_NEXT) = (double)(ph + 1);
       continue;
     }
     if (st && d < RTX_S_LEVELS) stat_add(st, RTX_S_HITS + d, 1);
-    Shade s;
-    shade_hit(sc, geo, mat, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s);
+    Hit s;
+    shade(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s);
     const bool weighted = s.lit && s.g != 0.0;
     bool descend = weighted && (B < 0 || d < B);
     if (descend && d + 1 >= p.stack_levels) {  // deeper than the stack: RecursionError on the host
@@ -568,17 +629,17 @@ __device__ void trace_general(const Params& p, const Stack& S, double ox0, doubl
       descend = false;
     }
     if (!descend) {
-      const double t_r = weighted ? (s.spec + 0.0) * s.g : 0.0;
-      S.at(d, F_AR) = S.at(d, F_AR) + ((s.ar + t_r) + s.ir);
-      S.at(d, F_AG) = S.at(d, F_AG) + ((s.ag + t_r) + s.ig);
-      S.at(d, F_AB) = S.at(d, F_AB) + ((s.ab + t_r) + s.ib);
+      double xr, xg, xb;
+      hit_color(mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.chk, s.lit, weighted, s.spec, s.va, 0.0, 0.0, 0.0, xr,
+                xg, xb);
+      S.at(d, F_AR) = S.at(d, F_AR) + xr;
+      S.at(d, F_AG) = S.at(d, F_AG) + xg;
+      S.at(d, F_AB) = S.at(d, F_AB) + xb;
       S.at(d, F_NEXT) = (double)(h + 1);
       continue;
     }
-    S.at(d, F_PAR) = s.ar; S.at(d, F_PAG) = s.ag; S.at(d, F_PAB) = s.ab;
-    S.at(d, F_PS) = s.spec; S.at(d, F_PG) = s.g;
-    S.at(d, F_PIR) = s.ir; S.at(d, F_PIG) = s.ig; S.at(d, F_PIB) = s.ib;
-    S.at(d, F_NEXT) = (double)h;
+    S.at(d, F_DLI) = s.dli; S.at(d, F_DI) = s.di; S.at(d, F_SPEC) = s.spec; S.at(d, F_VA) = s.va;
+    S.at(d, F_KEY) = (double)(h | (s.chk ? 0x10000 : 0));
     double rx = dx, ry = dy, rz = dz;
     reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
     ++d;
@@ -590,20 +651,31 @@ __device__ void trace_general(const Params& p, const Stack& S, double ox0, doubl
 
 __global__ __launch_bounds__(64) void k_render_general(Params p, int all_rays) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= p.n_workers) return;
-  const uint32_t* hdr = (const uint32_t*)p.ws;
+  uint32_t* hdr = (uint32_t*)p.ws;
   int64_t count = all_rays ? p.n : (int64_t)hdr[RTX_WS_COUNT];
   if (!all_rays && count > p.list_cap) count = p.list_cap;
   const int64_t* list = (const int64_t*)(p.ws + RTX_WS_HDR_BYTES);
-  Stack S{p.stack, p.n_workers, w};
-  for (int64_t item = w; item < count; item += p.n_workers) {
-    const int64_t i = all_rays ? item : list[item];
-    double ox, oy, oz, dx, dy, dz;
-    load_ray(p, i, ox, oy, oz, dx, dy, dz);
-    if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
-    double cr, cg, cb;
-    trace_general(p, S, ox, oy, oz, dx, dy, dz, cr, cg, cb);
-    write_out(p, i, cr, cg, cb);
+  if (w < p.n_workers) {
+    Stack S{p.stack, p.n_workers, w};
+    for (int64_t item = w; item < count; item += p.n_workers) {
+      const int64_t i = all_rays ? item : list[item];
+      double ox, oy, oz, dx, dy, dz;
+      load_ray(p, i, ox, oy, oz, dx, dy, dz);
+      if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
+      double cr, cg, cb;
+      trace_general(p, S, ox, oy, oz, dx, dy, dz, cr, cg, cb);
+      write_out(p, i, cr, cg, cb);
+    }
+  }
+  // leave the workspace clean for the next call: the last block to finish zeroes the counter
+  // (every block has read it before arriving; the next kernel on the stream sees the store)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = atomicAdd(hdr + RTX_WS_DONE, 1u);
+    if (prev == gridDim.x - 1) {
+      hdr[RTX_WS_COUNT] = 0u;
+      hdr[RTX_WS_DONE] = 0u;
+    }
   }
 }
 
@@ -616,7 +688,7 @@ __global__ __launch_bounds__(kBlock) void k_ray_dirs(Params p, double* __restric
   if (i >= p.n) return;
   const int lr = (int)(i / p.width), col = (int)(i % p.width);
   double dx, dy, dz;
-  camera_dir(p.scene, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
+  camera_dir((const cdouble*)p.scene, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
   out[i] = dx;
   out[p.n + i] = dy;
   out[2 * p.n + i] = dz;
@@ -690,10 +762,11 @@ int stack_levels_for(int max_bounces) {
 constexpr size_t kStackBudget = size_t(512) << 20;  // general-kernel frame stacks: <= 512 MiB
 constexpr int64_t kMaxWorkers = 65536;
 
-int64_t workers_for(int64_t n, int max_bounces) {
+int64_t workers_for(int64_t n, int max_bounces, bool deferred_only = false) {
   const size_t per = (size_t)stack_levels_for(max_bounces) * kFrameWords * sizeof(double);
   int64_t w = (int64_t)(kStackBudget / per);
   if (w > kMaxWorkers) w = kMaxWorkers;
+  if (deferred_only && w > kDeferredWorkers) w = kDeferredWorkers;
   const int64_t need = ((n + 63) / 64) * 64;
   if (w > need) w = need;
   w = (w / 64) * 64;
@@ -709,7 +782,12 @@ size_t ws_bytes(int64_t n, int max_bounces) {
 
 template <int B>
 void launch_fast_b(const Params& p, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_render_fast<B>, grid, dim3(kBlock), 0, s, p);
+  if (p.nsph <= kLdsMaxSpheres) {
+    const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double);
+    hipLaunchKernelGGL((k_render_fast<B, true>), grid, dim3(kBlock), lds, s, p);
+  } else {
+    hipLaunchKernelGGL((k_render_fast<B, false>), grid, dim3(kBlock), 0, s, p);
+  }
 }
 
 void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
@@ -738,10 +816,9 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.ws = (uint8_t*)workspace;
   p.list_cap = p.n;
   p.stack = (double*)(p.ws + RTX_WS_HDR_BYTES + ((list_bytes(p.n) + 255) / 256) * 256);
-  p.n_workers = workers_for(p.n, p.max_bounces);
-  p.stack_levels = stack_levels_for(p.max_bounces);
-  if (hipMemsetAsync(workspace, 0, RTX_WS_HDR_BYTES, s) != hipSuccess) return check_launch("hipMemsetAsync");
   const bool fast = p.max_bounces >= 0 && p.max_bounces <= RTX_FAST_MAX_BOUNCES;
+  p.n_workers = workers_for(p.n, p.max_bounces, fast);
+  p.stack_levels = stack_levels_for(p.max_bounces);
   if (fast) {
     dim3 grid;
     if (p.mode == 0) {

@@ -223,7 +223,8 @@ class HipRenderer(Renderer):
     def workspace(self, n: int) -> torch.Tensor:
         need = int(self._lib.rtx_workspace_bytes(int(n), self._bounces_arg))
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            # zero-filled once; every call leaves its counters zeroed again (include/rtx_hip.h)
+            self._ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
     def _stats_ptr(self):
@@ -232,6 +233,8 @@ class HipRenderer(Renderer):
     def _check_status(self, ws: torch.Tensor) -> None:
         if self.max_bounces is None or self.max_bounces > L.FAST_MAX_BOUNCES:
             status = int(ws[:8].view(torch.int32)[1].item())
+            if status:
+                ws[4:8].zero_()  # sticky flags: clear for the next call
             if status & L.ST_STACK_OVERFLOW:
                 raise RecursionError(f"maximum recursion depth exceeded (reflection chain > {L.UNBOUNDED_LEVELS} levels)")
 
