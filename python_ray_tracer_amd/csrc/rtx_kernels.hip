@@ -42,12 +42,20 @@
 namespace {
 
 constexpr int kBlock = 256;   // 4 waves
-constexpr int kTileW = 16;    // block tile: 16 x 16 pixels, each wave an 8 x 8 sub-tile
-constexpr int kTileH = 16;
+#ifndef RTX_WAVE_W
+#define RTX_WAVE_W 8  // pixels per wave row: a wave renders an RTX_WAVE_W x (64 / RTX_WAVE_W) tile
+#endif
+constexpr int kWaveW = RTX_WAVE_W;
+constexpr int kWaveH = 64 / kWaveW;
+constexpr int kTileW = 2 * kWaveW;  // block tile: 2 x 2 waves
+constexpr int kTileH = 2 * kWaveH;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
 constexpr int kDeferredWorkers = 4096;  // general-kernel threads when it only serves ties
+#ifndef RTX_FAST_WAVES
+#define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
+#endif
 
 // Wave-uniform loads through the scalar cache: the constant address space makes hipcc emit s_load
 // even though the kernel also stores (it cannot prove the scene blob is not aliased otherwise).
@@ -198,6 +206,21 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   return (NdotV <= 0.0) ? 0.0 : sf;  // :318
 }
 
+#ifdef RTX_IRID_CALL
+__device__ __attribute__((noinline)) void irid_terms(double va, double tft, double hs, double omhs, double w,
+                                                     double igain, double& ir, double& ig, double& ib) {
+  const double af = fabs(va - 0.5) * 2.0;  // :204
+  const double phase = ((af * RTX_PI) * tft) * 10.0;  // :208
+  const double ip = sin(phase);  // :211
+  const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
+  const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222
+  const double b = 0.5 + 0.5 * ip;  // :223
+  ir = (r * w) * igain;  // :229-232
+  ig = (gg * w) * igain;
+  ib = (b * w) * igain;
+}
+#endif
+
 // Colour of one shaded hit given the reflected colour R (shader.py:86-110):
 //   ((((0.004 + diffuse) + dome) + (spec + R*0.5)*g*lit) + irid)
 // `weighted` = lit && g != 0; otherwise the specular/reflection term is x*0 == 0 (R is finite).
@@ -228,9 +251,18 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   double ir = 0.0, ig = 0.0, ib = 0.0;
   const double igain = mh[RTX_M_IG];
   if (igain != 0.0) {
+#ifdef RTX_IRID_CALL
+    irid_terms(va, mh[RTX_M_TFT], mh[RTX_M_HS], mh[RTX_M_1MHS], mh[RTX_M_TFW], igain, ir, ig, ib);
+  }
+  if (false) {
+#endif
     const double af = fabs(va - 0.5) * 2.0;  // :204
     const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
+#ifdef RTX_ABL_SIN  // timing ablation only (wrong output)
+    const double ip = phase * 0.1;
+#else
     const double ip = sin(phase);  // :211
+#endif
     const double hs = mh[RTX_M_HS], omhs = mh[RTX_M_1MHS];
     const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
     const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222
@@ -268,7 +300,12 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
   const double qq = dot3(qx, qy, qz, qx, qy, qz);
   const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
   bool lit = true;
+#ifdef RTX_ABL_SHADOW  // timing ablation only (wrong output)
+  lit = tself > 1.0;
+  for (int j = 0; j < 0; ++j) {
+#else
   for (int j = 0; j < nsph; ++j) {
+#endif
     const int ju = __builtin_amdgcn_readfirstlane(j);
     if (isect(geo + ju * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz) < tself) {
       lit = false;
@@ -290,7 +327,11 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
   if (weighted || need_irid) {
     double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
     norm3(vx, vy, vz);  // :76 (towards the camera on every level)
+#ifdef RTX_ABL_SPEC  // timing ablation only (wrong output)
+    if (weighted) spec = vx * lx + vy;
+#else
     if (weighted) spec = specular(mh, g, nx, ny, nz, lx, ly, lz, vx, vy, vz);
+#endif
     if (need_irid) va = clip01(dot3(nx, ny, nz, vx, vy, vz));  // :201
   }
   s.dli = dli;
@@ -397,7 +438,7 @@ __device__ __forceinline__ void stat_add(unsigned long long* st, int word, unsig
 // ------------------------------------------------------------------------------------------
 
 template <int B, bool LDS>
-__global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
+__global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
@@ -411,10 +452,10 @@ __global__ __launch_bounds__(kBlock) void k_render_fast(Params p) {
 
   int64_t i;
   if (p.mode == 0) {
-    // 16x16 block tile; wave w -> 8x8 sub-tile, lane -> (l & 7, l >> 3)
+    // 2x2 waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = blockIdx.x * kTileW + (w & 1) * 8 + (lane & 7);
-    const int lr = blockIdx.y * kTileH + (w >> 1) * 8 + (lane >> 3);
+    const int col = blockIdx.x * kTileW + (w & 1) * kWaveW + (lane % kWaveW);
+    const int lr = blockIdx.y * kTileH + (w >> 1) * kWaveH + (lane / kWaveW);
     if (col >= p.width || lr >= p.n_rows) return;
     i = (int64_t)lr * p.width + col;
   } else {
