@@ -130,7 +130,9 @@ enum {
   RTX_S_LEVELS = 64,  /* levels recorded                        */
   RTX_S_RAYS = 8,     /* [8 .. 8+64): rays traced per level     */
   RTX_S_HITS = 72,    /* [72 .. 72+64): shaded hits (= shadow rays) per level */
-  RTX_S_WORDS = 136
+  RTX_S_WTRACE = 136, /* [136 .. 136+64): waves that traced a level (any lane live), fast kernel */
+  RTX_S_WSHADE = 200, /* [200 .. 200+64): waves that shaded a level (any lane hit), fast kernel  */
+  RTX_S_WORDS = 264
 };
 
 /* workspace: status words then deferred-ray list then per-worker frame stacks.
@@ -190,6 +192,12 @@ int rtx_sphere_intersect(const double* sphere, const double* origins, int64_t or
 /* save_image's quantisation (base.py:143-151): color [3][n] (RTX_OUT_F32_SOA or _F64_SOA) ->
  * out [n][3] uint8 = (uint8)(255 * clip(c, 0, 1)). */
 int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, void* stream);
+
+/* Test hook: out[0:n] = the library's fast-path sqrt(a), out[n:2n] = the compiler's full sqrt(a),
+ * out[2n:3n] = fast-path a/b, out[3n:4n] = full a/b. The render kernels use the fast paths
+ * (correctly rounded sequences without operand scaling where it is the identity); tests require
+ * each pair to agree bit for bit. */
+int rtx_selftest_math(const double* a, const double* b, int64_t n, double* out, void* stream);
 
 /* Live timing of the dominant render kernel (used by bench.py for the roofline): after
  * rtx_profile_enable(k), the next k render launches record a hipEvent pair on their stream around

@@ -17,7 +17,10 @@ LIB = PKG / "librtx_hip.so"
 # -ffp-contract=off: NumPy never fuses a*b+c, and FMA contraction would move linspace / checker
 # boundaries. No fast-math: sqrt and division stay correctly rounded.
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-function"]
+               "-Wall", "-Wno-unused-function", "-Wno-unused-result",
+               # MachineLICM hoists the ocml sin polynomial constants out of the bounce loop into VGPRs,
+               # which then spill at 128 VGPRs; A/B (profiles/r1_ab_variants.txt): faster on every config
+               "-mllvm", "-disable-machine-licm"]
 
 
 def hipcc() -> str:

@@ -92,24 +92,64 @@ __device__ __forceinline__ double dot3(double ax, double ay, double az, double b
   return ((ax * bx) + (ay * by)) + (az * bz);  // NumpyVector3D.dot, base.py:34-35
 }
 
+// Correctly rounded sqrt and division, fast paths. LLVM lowers f64 sqrt / fdiv for gfx9 to a
+// correctly rounded sequence (v_rsq_f64 / v_rcp_f64 + Newton-Raphson FMAs) wrapped in operand
+// scaling (v_ldexp, v_div_scale) and special-value fix-ups (v_cmp_class, v_div_fixup). For operands
+// where the scaling is provably the identity and no special value occurs, the cores below are the
+// very same instruction sequence without the wrapping, hence bit-identical; every other operand
+// takes the full expansion. (k_selftest_math checks both paths bit for bit on the device.)
+__device__ __forceinline__ double sqrt_core(double x) {  // x in [2^-767, DBL_MAX]
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double sqrt_cr(double x) {
+  if (x >= 0x1.0p-767 && x <= 0x1.fffffffffffffp+1023) return sqrt_core(x);
+  return __builtin_sqrt(x);
+}
+// a / b for a, b with |.| in [2^-300, 2^300] (v_div_scale leaves them unchanged and clears VCC, so
+// v_div_fmas is a plain fma; the quotient is normal, so v_div_fixup returns it unchanged)
+__device__ __forceinline__ double div_core(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = a * r;
+  const double rem = __builtin_fma(-b, q, a);
+  return __builtin_fma(rem, r, q);
+}
+__device__ __forceinline__ bool div_range(double x) {
+  const double ax = fabs(x);
+  return ax >= 0x1.0p-300 && ax <= 0x1.0p+300;
+}
+__device__ __forceinline__ double div_cr(double a, double b) {
+  if (div_range(b) && (a == 0.0 || div_range(a))) return a == 0.0 ? a * __builtin_copysign(1.0, b) : div_core(a, b);
+  return a / b;
+}
+
 __device__ __forceinline__ void norm3(double& x, double& y, double& z) {
   // NumpyVector3D.norm, base.py:61-64: v * (1.0 / where(mag == 0, 1, mag))
-  const double mag = sqrt(dot3(x, y, z, x, y, z));
-  const double r = 1.0 / (mag == 0.0 ? 1.0 : mag);
+  const double mag = sqrt_cr(dot3(x, y, z, x, y, z));
+  const double r = div_cr(1.0, mag == 0.0 ? 1.0 : mag);
   x = x * r;
   y = y * r;
   z = z * r;
 }
 
-__device__ __forceinline__ double clip01(double x) {
-  // np.clip(x, 0, 1) (NaN propagates)
-  return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
-}
+// np.clip(x, 0, 1) and np.maximum(x, 0) as v_max_f64 / v_min_f64. They differ from the reference
+// only for NaN inputs and in the sign of a zero result, which never reaches the output: every such
+// value is squared, scaled into a sum with the 0.004 ambient term, or compared with <= 0.
+__device__ __forceinline__ double clip01(double x) { return __builtin_fmin(__builtin_fmax(x, 0.0), 1.0); }
 
-__device__ __forceinline__ double max0(double x) {
-  // np.maximum(x, 0)
-  return x < 0.0 ? 0.0 : x;
-}
+__device__ __forceinline__ double max0(double x) { return __builtin_fmax(x, 0.0); }
 
 __device__ __forceinline__ int trunc_parity(double x) {
   // (x).astype(int) % 2 (shader.py:30): truncation to int64, then floor-mod 2 == (k & 1).
@@ -130,30 +170,100 @@ __device__ __forceinline__ double isect(const P* g, double ox, double oy, double
   const double disc = (b * b) - (4.0 * c);
   double t = FARAWAY;
   if (disc > 0.0) {  // np.where((disc > 0) & (sol > 0), sol, FARAWAY); sqrt(max(0, disc)) == sqrt(disc) here
-    const double sq = sqrt(disc);
+    const double sq = sqrt_cr(disc);
     const double s0 = (-b - sq) * 0.5;  // == / 2 exactly
     const double s1 = (-b + sq) * 0.5;
-    const double sol = (s0 > 0.0 && s0 < s1) ? s0 : s1;
+    // (s0 > 0) & (s0 < s1) ? s0 : s1 — with sq > 0, s0 <= s1 and s0 == s1 only as equal values
+    const double sol = s0 > 0.0 ? s0 : s1;
     if (sol > 0.0) t = sol;
   }
   return t;
 }
 
-// Same, level-0 camera origin: O - C and c precomputed with the same expressions (host: c, here
-// O - C from uniform values).
-__device__ __forceinline__ double isect_cam(const cdouble* g, double ocx, double ocy, double ocz, double dx, double dy,
-                                            double dz) {
-  const double b = 2.0 * dot3(dx, dy, dz, ocx, ocy, ocz);
-  const double disc = (b * b) - (4.0 * g[RTX_G_C0]);
-  double t = FARAWAY;
-  if (disc > 0.0) {
-    const double sq = sqrt(disc);
-    const double s0 = (-b - sq) * 0.5;
-    const double s1 = (-b + sq) * 0.5;
-    const double sol = (s0 > 0.0 && s0 < s1) ? s0 : s1;
-    if (sol > 0.0) t = sol;
+// The same test split in two halves so that two spheres' dependency chains interleave (and their
+// scalar loads share one wait): isect_disc computes b and the discriminant, isect_roots the rest.
+template <typename P>
+__device__ __forceinline__ void isect_disc(const P* g, double ox, double oy, double oz, double oo, double dx,
+                                           double dy, double dz, double& b, double& disc) {
+  const double cx = g[RTX_G_CX], cy = g[RTX_G_CY], cz = g[RTX_G_CZ];
+  b = 2.0 * dot3(dx, dy, dz, ox - cx, oy - cy, oz - cz);
+  const double c = ((g[RTX_G_CC] + oo) - 2.0 * dot3(cx, cy, cz, ox, oy, oz)) - g[RTX_G_RR];
+  disc = (b * b) - (4.0 * c);
+}
+// level-0 camera origin: O - C from uniform values, c precomputed on the host (same expressions)
+__device__ __forceinline__ void isect_disc_cam(const cdouble* g, double ox, double oy, double oz, double dx, double dy,
+                                               double dz, double& b, double& disc) {
+  b = 2.0 * dot3(dx, dy, dz, ox - g[RTX_G_CX], oy - g[RTX_G_CY], oz - g[RTX_G_CZ]);
+  disc = (b * b) - (4.0 * g[RTX_G_C0]);
+}
+__device__ __forceinline__ double isect_roots(double b, double disc) {
+  // disc <= 0 lanes compute a dummy root (discarded below) so that every lane stays on sqrt_cr's
+  // fast path
+  const double sq = sqrt_cr(disc > 0.0 ? disc : 1.0);
+  const double s0 = (-b - sq) * 0.5;
+  const double s1 = (-b + sq) * 0.5;
+  const double sol = s0 > 0.0 ? s0 : s1;  // see isect
+  return (disc > 0.0 && sol > 0.0) ? sol : FARAWAY;
+}
+// two spheres at once; the square roots run only if either discriminant is positive (per lane)
+__device__ __forceinline__ void isect_pair_roots(double b0, double disc0, double b1, double disc1, double& t0,
+                                                 double& t1) {
+  t0 = FARAWAY;
+  t1 = FARAWAY;
+  if (disc0 > 0.0 || disc1 > 0.0) {
+    t0 = isect_roots(b0, disc0);
+    t1 = isect_roots(b1, disc1);
   }
-  return t;
+}
+
+// nearest-hit bookkeeping in scene order (base.py:97-103): the first strictly smaller t wins; an
+// equal t (not FARAWAY) marks a tie, which is cleared by any later strictly smaller t
+__device__ __forceinline__ void nearest_update(double t, int s, double& tmin, int& hit, bool& tie) {
+  if (t < tmin) {
+    tmin = t;
+    hit = s;
+    tie = false;
+  } else if (t == tmin && t != FARAWAY) {
+    tie = true;
+  }
+}
+
+// Nearest hit of ray (O, D) over all spheres; wave-uniform loop over sphere pairs, geometry through
+// the scalar cache. CAM: O is the camera (level 0), using the host-precomputed c.
+template <bool CAM>
+__device__ __forceinline__ void nearest_hit(const cdouble* geo, int nsph, double ox, double oy, double oz, double dx,
+                                            double dy, double dz, double& tmin, int& hit, bool& tie) {
+  tmin = FARAWAY;
+  hit = -1;
+  tie = false;
+  const double oo = CAM ? 0.0 : dot3(ox, oy, oz, ox, oy, oz);
+  int s = 0;
+  for (; s + 1 < nsph; s += 2) {
+    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const cdouble* g1 = g0 + RTX_GEOM_WORDS;
+    double b0, d0, b1, d1;
+    if (CAM) {
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
+      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1);
+    } else {
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1);
+    }
+    double t0, t1;
+    isect_pair_roots(b0, d0, b1, d1, t0, t1);
+    nearest_update(t0, s, tmin, hit, tie);
+    nearest_update(t1, s + 1, tmin, hit, tie);
+  }
+  if (s < nsph) {
+    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    double b0, d0;
+    if (CAM) {
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
+    } else {
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+    }
+    nearest_update(d0 > 0.0 ? isect_roots(b0, d0) : FARAWAY, s, tmin, hit, tie);
+  }
 }
 
 // (x)^5 and (x)^2.5 for x in [0, 1] (shader.py:291, :310). NumPy evaluates these with its SIMD pow;
@@ -162,7 +272,7 @@ __device__ __forceinline__ double pow5(double x) {
   const double x2 = x * x;
   return (x2 * x2) * x;
 }
-__device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt(x); }
+__device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt_cr(x); }
 
 // The inputs of one shaded hit's colour terms (everything else comes from the material record).
 struct Hit {
@@ -195,12 +305,12 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
   const double a2 = mh[RTX_M_A2];
   const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
-  const double D = a2 / (RTX_PI * ((denom * denom) + 1e-8));  // :296
+  const double D = div_cr(a2, RTX_PI * ((denom * denom) + 1e-8));  // :296
   const double oma2 = mh[RTX_M_1MA2];
-  const double G1L = (2.0 * NdotL) / ((NdotL + sqrt(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
-  const double G1V = (2.0 * NdotV) / ((NdotV + sqrt(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
+  const double G1L = div_cr(2.0 * NdotL, (NdotL + sqrt_cr(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
+  const double G1V = div_cr(2.0 * NdotV, (NdotV + sqrt_cr(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
   const double G = G1L * G1V;  // :303
-  const double spec_base = ((F * D) * G) / ((4.0 * NdotV) + 1e-8);  // :306
+  const double spec_base = div_cr((F * D) * G, (4.0 * NdotV) + 1e-8);  // :306
   const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
   const double sf = spec_base + g * glint;  // :315
   return (NdotV <= 0.0) ? 0.0 : sf;  // :318
@@ -302,15 +412,28 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
   bool lit = true;
 #ifdef RTX_ABL_SHADOW  // timing ablation only (wrong output)
   lit = tself > 1.0;
-  for (int j = 0; j < 0; ++j) {
+  const int nshadow = 0;
 #else
-  for (int j = 0; j < nsph; ++j) {
+  const int nshadow = nsph;
 #endif
-    const int ju = __builtin_amdgcn_readfirstlane(j);
-    if (isect(geo + ju * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz) < tself) {
+  int j = 0;
+  for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
+    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
+    const cdouble* g1 = g0 + RTX_GEOM_WORDS;
+    double b0, d0, b1, d1, t0, t1;
+    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+    isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
+    isect_pair_roots(b0, d0, b1, d1, t0, t1);
+    if (t0 < tself || t1 < tself) {
       lit = false;
       break;
     }
+  }
+  if (lit && j < nshadow) {
+    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
+    double b0, d0;
+    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+    if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
   }
 
   const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));  // :138
@@ -375,8 +498,8 @@ __device__ __forceinline__ void camera_dir(const cdouble* sc, int col, int r, in
   const double vx = x - sc[RTX_H_CAM + 0];
   const double vy = y - sc[RTX_H_CAM + 1];
   const double vz = sc[RTX_H_VZ];
-  const double mag = sqrt(((vx * vx) + (vy * vy)) + sc[RTX_H_VZ2]);
-  const double rr = 1.0 / (mag == 0.0 ? 1.0 : mag);
+  const double mag = sqrt_cr(((vx * vx) + (vy * vy)) + sc[RTX_H_VZ2]);
+  const double rr = div_cr(1.0, mag == 0.0 ? 1.0 : mag);
   dx = vx * rr;
   dy = vy * rr;
   dz = vz * rr;
@@ -433,6 +556,12 @@ __device__ __forceinline__ void stat_add(unsigned long long* st, int word, unsig
   atomicAdd(st + word, v);
 }
 
+// one count per wave (from its first active lane): how many waves execute a stage
+__device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
+  const unsigned long long m = __ballot(1);
+  if ((int)__lane_id() == __ffsll((long long)m) - 1) atomicAdd(st + word, 1ull);
+}
+
 // ------------------------------------------------------------------------------------------
 // k_render_fast<B, LDS>
 // ------------------------------------------------------------------------------------------
@@ -477,36 +606,18 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
   bool deferred = false;
 
   for (int k = 0;; ++k) {
-    if (st && k < RTX_S_LEVELS) stat_add(st, RTX_S_RAYS + k, 1);
+    if (st && k < RTX_S_LEVELS) {
+      stat_add(st, RTX_S_RAYS + k, 1);
+      stat_wave(st, RTX_S_WTRACE + k);
+    }
     // nearest hit over all shapes (base.py:97-103), wave-uniform loop, geometry via s_load
-    double tmin = FARAWAY;
-    int hit = -1;
-    bool tie = false;
+    double tmin;
+    int hit;
+    bool tie;
     if (k == 0 && cam0) {
-      for (int s = 0; s < nsph; ++s) {
-        const cdouble* gs = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
-        const double t = isect_cam(gs, ox - gs[RTX_G_CX], oy - gs[RTX_G_CY], oz - gs[RTX_G_CZ], dx, dy, dz);
-        if (t < tmin) {
-          tmin = t;
-          hit = s;
-          tie = false;
-        } else if (t == tmin && t != FARAWAY) {
-          tie = true;
-        }
-      }
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
     } else {
-      const double oo = dot3(ox, oy, oz, ox, oy, oz);
-      for (int s = 0; s < nsph; ++s) {
-        const cdouble* gs = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
-        const double t = isect(gs, ox, oy, oz, oo, dx, dy, dz);
-        if (t < tmin) {
-          tmin = t;
-          hit = s;
-          tie = false;
-        } else if (t == tmin && t != FARAWAY) {
-          tie = true;
-        }
-      }
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
     }
     if (hit < 0) {  // nothing hit: NumpyRGBColor(0, 0, 0) (base.py:100)
       cr = cg = cb = 0.0;
@@ -517,7 +628,10 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
       if (st) stat_add(st, RTX_S_TIES, 1);
       break;
     }
-    if (st && k < RTX_S_LEVELS) stat_add(st, RTX_S_HITS + k, 1);
+    if (st && k < RTX_S_LEVELS) {
+      stat_add(st, RTX_S_HITS + k, 1);
+      stat_wave(st, RTX_S_WSHADE + k);
+    }
     Hit s;
     if constexpr (LDS) {
       shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
@@ -744,6 +858,18 @@ __global__ __launch_bounds__(kBlock) void k_intersect(const double* __restrict__
   const double ox = org[j], oy = org[s + j + (s ? 0 : 1)], oz = org[2 * s + j + (s ? 0 : 2)];
   const double dx = dir[i], dy = dir[n + i], dz = dir[2 * n + i];
   t[i] = isect(g, ox, oy, oz, dot3(ox, oy, oz, ox, oy, oz), dx, dy, dz);
+}
+
+// bit-exactness check of the sqrt / division fast paths against the compiler's full expansions
+__global__ __launch_bounds__(kBlock) void k_selftest_math(const double* __restrict__ a, const double* __restrict__ b,
+                                                          int64_t n, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double x = a[i], y = b[i];
+  out[i] = sqrt_cr(x);
+  out[n + i] = __builtin_sqrt(x);
+  out[2 * n + i] = div_cr(x, y);
+  out[3 * n + i] = x / y;
 }
 
 template <typename T>
@@ -1010,6 +1136,14 @@ int rtx_sphere_intersect(const double* sphere, const double* origins, int64_t or
   hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
                      sphere, origins, origin_stride, dirs, n, t_out);
   return check_launch("k_intersect");
+}
+
+int rtx_selftest_math(const double* a, const double* b, int64_t n, double* out, void* stream) {
+  if (!a || !b || !out) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (n <= 0) return RTX_OK;
+  hipLaunchKernelGGL(k_selftest_math, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a, b, n, out);
+  return check_launch("k_selftest_math");
 }
 
 int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, void* stream) {

@@ -22,7 +22,7 @@ HDR_WORDS = 64
 GEOM_WORDS = 8
 MAT_WORDS = 24
 MAX_DOMES = 8
-S_WORDS = 136
+S_WORDS = 264
 WS_HDR_BYTES = 256
 FAST_MAX_BOUNCES = 8
 UNBOUNDED_LEVELS = 333
@@ -48,7 +48,7 @@ G_CX, G_CY, G_CZ, G_CC, G_RR, G_INVR, G_C0 = 0, 1, 2, 3, 4, 5, 6
 (M_G, M_DG, M_TEX, M_TR, M_TG, M_TB, M_A2, M_A2M1, M_1MA2, M_F0, M_1MF0, M_IG, M_TFW, M_TFT, M_HS, M_1MHS,
  M_ROUGH, M_REFL, M_IOR, M_TFIOR) = range(20)
 # stats words
-S_PIXELS, S_DEFERRED, S_TIES, S_RAYS, S_HITS, S_LEVELS = 0, 1, 2, 8, 72, 64
+S_PIXELS, S_DEFERRED, S_TIES, S_RAYS, S_HITS, S_LEVELS, S_WTRACE, S_WSHADE = 0, 1, 2, 8, 72, 64, 136, 200
 
 EXPORTS = (
     "rtx_abi_version",
@@ -61,6 +61,7 @@ EXPORTS = (
     "rtx_quantize_u8",
     "rtx_profile_enable",
     "rtx_profile_collect",
+    "rtx_selftest_math",
 )
 
 _c_void_p = ctypes.c_void_p
@@ -81,6 +82,7 @@ _SIGS = {
     "rtx_quantize_u8": (_i32, [_c_void_p, _i32, _i64, _c_void_p, _c_void_p]),
     "rtx_profile_enable": (_i32, [_i32]),
     "rtx_profile_collect": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
+    "rtx_selftest_math": (_i32, [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
 }
 
 _lib = None

@@ -351,7 +351,8 @@ class HipRenderer(Renderer):
         hits = s[L.S_HITS:L.S_HITS + L.S_LEVELS]
         last = max([i + 1 for i, v in enumerate(rays) if v] or [0])
         return {"pixels": s[L.S_PIXELS], "deferred": s[L.S_DEFERRED], "ties": s[L.S_TIES],
-                "rays": rays[:last], "hits": hits[:last]}
+                "rays": rays[:last], "hits": hits[:last],
+                "waves_traced": s[L.S_WTRACE:L.S_WTRACE + last], "waves_shaded": s[L.S_WSHADE:L.S_WSHADE + last]}
 
     def reset_stats(self) -> None:
         if self.stats_buffer is not None:

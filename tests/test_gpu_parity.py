@@ -149,6 +149,37 @@ def test_explicit_rays_and_intersect(hip, golden_meta):
         assert float(t[0]) == k["t"], k["label"]
 
 
+def test_fast_sqrt_div_bit_exact(hip):
+    """The kernels' sqrt / division fast paths equal the compiler's full correctly-rounded
+    expansions bit for bit, and both equal the CPU's IEEE sqrt and division."""
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    e = rng.uniform(-320, 320, n)
+    a = rng.uniform(0.5, 1.0, n) * np.exp2(np.round(e))
+    b = rng.uniform(0.5, 1.0, n) * np.exp2(np.round(rng.uniform(-320, 320, n))) * np.where(rng.random(n) < 0.5, -1, 1)
+    specials = np.array([0.0, -0.0, 1.0, 4.0, 1e-8, 2.0 ** -767, 2.0 ** -768, 2.0 ** -300, 2.0 ** 300, 1e-310,
+                         np.finfo(float).max, np.inf, 0.9999999999999999, 1.0000000000000002])
+    a[:specials.size] = specials
+    b[:specials.size] = specials[::-1]
+    a[specials.size:2 * specials.size] = np.abs(rng.normal(size=specials.size)) * 1e-8
+    A = torch.from_numpy(a).cuda()
+    Bt = torch.from_numpy(b).cuda()
+    out = torch.empty(4 * n, dtype=torch.float64, device="cuda")
+    L.check(L.load().rtx_selftest_math(A.data_ptr(), Bt.data_ptr(), n, out.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream), "rtx_selftest_math")
+    o = out.cpu().numpy().reshape(4, n).view(np.uint64)
+    assert np.array_equal(o[0], o[1]), "fast sqrt != full sqrt"
+    assert np.array_equal(o[2], o[3]), "fast div != full div"
+    with np.errstate(all="ignore"):
+        pos = a >= 0
+        assert np.array_equal(o[1][pos], np.sqrt(a[pos]).view(np.uint64))
+        q = a / b
+        fin = np.isfinite(q)
+        assert np.array_equal(o[3][fin], q[fin].view(np.uint64))
+
+
 def test_quantize_matches_numpy(hip):
     r = hip.HipRenderer(max_bounces=1)
     vals = np.concatenate([np.linspace(-0.5, 1.5, 4001), [0, 1, 1 / 255, 2 / 255, 254.99999 / 255, np.inf, -np.inf]])

@@ -25,6 +25,8 @@ from python_ray_tracer_amd.infrastructure.hip.scene_pack import pack_scene  # no
 def open_lib(path):
     lib = ctypes.CDLL(str(Path(path).resolve()))
     for name, (res, args) in L._SIGS.items():
+        if not hasattr(lib, name):  # older builds lack newer entry points
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
