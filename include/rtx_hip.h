@@ -75,7 +75,12 @@ enum {
   RTX_H_VZ2 = 29,    /* VZ*VZ */
   RTX_H_W = 30,
   RTX_H_H = 31,
-  RTX_H_CAMOO = 32   /* |camera|^2 = camera.dot(camera) (shape.py:35 with the level-0 origin) */
+  RTX_H_CAMOO = 32,  /* |camera|^2 = camera.dot(camera) (shape.py:35 with the level-0 origin) */
+  /* optional culling hierarchy (RTX_H_NNODES == 0: none, every ray tests every sphere) */
+  RTX_H_NNODES = 33, /* bounding-sphere tree nodes, depth-first order                        */
+  RTX_H_NALWAYS = 34,/* leading entries of the culled geometry list tested by every ray (huge spheres) */
+  RTX_H_NODES = 35,  /* word offset of the node array (RTX_NODE_WORDS each)                 */
+  RTX_H_CGEO = 36    /* word offset of the culled geometry list (S records, RTX_GEOM_WORDS)  */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 
@@ -85,7 +90,22 @@ enum {
   RTX_G_CC = 3,    /* abs(position) = C.C                 (shape.py:35)  */
   RTX_G_RR = 4,    /* radius*radius                       (shape.py:36)  */
   RTX_G_INVR = 5,  /* 1.0/radius                          (shader.py:74) */
-  RTX_G_C0 = 6     /* c for the camera origin: ((C.C + O.O) - 2*C.O) - r*r, O = camera */
+  RTX_G_C0 = 6,    /* c for the camera origin: ((C.C + O.O) - 2*C.O) - r*r, O = camera */
+  RTX_G_IDX = 7    /* scene index of the sphere (culled geometry list only)              */
+};
+
+/* culling-tree node words. A node bounds all spheres below it; the tree is stored depth-first
+ * with a skip link, so a wave traverses it without a stack. A node is entered when any lane of
+ * the wave may hit its bound (conservative test, see rtx_kernels.hip: a skipped sphere is one the
+ * reference formula provably reports as FARAWAY); leaves list their spheres as a range of the
+ * culled geometry list. */
+enum {
+  RTX_NODE_WORDS = 8,
+  RTX_N_CX = 0, RTX_N_CY = 1, RTX_N_CZ = 2, RTX_N_R = 3,
+  RTX_N_FIRST = 4,  /* leaf: first culled-geometry entry   */
+  RTX_N_COUNT = 5,  /* leaf: sphere count (0: inner node)  */
+  RTX_N_SKIP = 6,   /* node index after this subtree        */
+  RTX_N_CC = 7      /* (|Cn| + R)^2, bounds |C|^2 of every sphere below (error budget) */
 };
 
 /* per-sphere material words (NumpyShader, shader.py:36-54; derived constants computed on the

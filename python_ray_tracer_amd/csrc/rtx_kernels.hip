@@ -53,6 +53,12 @@ constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
 constexpr int kDeferredWorkers = 4096;  // general-kernel threads when it only serves ties
+// geometry source of the wave-uniform sphere loops after level 0 (LDS variant: the LDS table)
+#ifdef RTX_GEO_LDS
+#define RTX_LOOP_GEO ((const double*)lds_tab)
+#else
+#define RTX_LOOP_GEO geo
+#endif
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
 #endif
@@ -82,6 +88,7 @@ struct Params {
   int64_t n_workers;
   int stack_levels;
   unsigned long long* stats;
+  int n_tiles_x, n_tiles_y;  // persistent launch of k_render_fast (0: one tile per block)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -191,7 +198,8 @@ __device__ __forceinline__ void isect_disc(const P* g, double ox, double oy, dou
   disc = (b * b) - (4.0 * c);
 }
 // level-0 camera origin: O - C from uniform values, c precomputed on the host (same expressions)
-__device__ __forceinline__ void isect_disc_cam(const cdouble* g, double ox, double oy, double oz, double dx, double dy,
+template <typename P>
+__device__ __forceinline__ void isect_disc_cam(const P* g, double ox, double oy, double oz, double dx, double dy,
                                                double dz, double& b, double& disc) {
   b = 2.0 * dot3(dx, dy, dz, ox - g[RTX_G_CX], oy - g[RTX_G_CY], oz - g[RTX_G_CZ]);
   disc = (b * b) - (4.0 * g[RTX_G_C0]);
@@ -228,10 +236,142 @@ __device__ __forceinline__ void nearest_update(double t, int s, double& tmin, in
   }
 }
 
+// ---- culling hierarchy ---------------------------------------------------------------------
+// Conservative test: may any sphere inside the bound (centre Cn, radius R) produce, through the
+// reference formula (shape.py:34-51), a hit with 0 < t <= tlim? If this returns false, every such
+// sphere provably yields FARAWAY (or a t > tlim), so skipping it changes neither the nearest hit nor
+// the tie test nor the shadow test. Error budget: the reference's discriminant is computed with an
+// absolute error err <= ~64 eps * scale, scale = |Cn-O|^2 + (|Cn|+R)^2 + |O|^2 + R^2 (cancellation
+// in c = |C|^2 + |O|^2 - 2 C.O - r^2); through the square root a root moves by <= sqrt(err)
+// <= 1e-7 (scale + 1); the perpendicular distance by as much. Both margins below exceed that by a
+// wide factor, and |D| = 1 +- 1e-15 is absorbed too.
+__device__ __forceinline__ bool node_may_hit(const cdouble* nd, double ox, double oy, double oz, double oo, double dx,
+                                             double dy, double dz, double tlim) {
+  const double ocx = nd[RTX_N_CX] - ox, ocy = nd[RTX_N_CY] - oy, ocz = nd[RTX_N_CZ] - oz;
+  const double R = nd[RTX_N_R];
+  const double tca = dot3(ocx, ocy, ocz, dx, dy, dz);
+  const double oc2 = dot3(ocx, ocy, ocz, ocx, ocy, ocz);
+  const double scale = ((oc2 + nd[RTX_N_CC]) + oo) + R * R + 1.0;
+  const double lm = 1e-7 * scale;                      // distance margin
+  const double line = oc2 - tca * tca;                 // squared distance of Cn from the ray's line
+  const double rl = R + lm;
+  return line <= rl * rl && tca + R >= -lm && tca - R - lm <= tlim;
+}
+
+// Nearest hit over entries [first, first + cnt) of the culled geometry list (pairs, scalar loads).
+template <bool CAM>
+__device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int cnt, double ox, double oy, double oz,
+                                              double oo, double dx, double dy, double dz, double& tmin, int& hit,
+                                              bool& tie) {
+  const int end = first + cnt;
+  int k = first;
+  for (; k + 1 < end; k += 2) {
+    const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+    const cdouble* g1 = g0 + RTX_GEOM_WORDS;
+    double b0, d0, b1, d1, t0, t1;
+    if (CAM) {
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
+      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1);
+    } else {
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1);
+    }
+    isect_pair_roots(b0, d0, b1, d1, t0, t1);
+    nearest_update(t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
+    nearest_update(t1, (int)g1[RTX_G_IDX], tmin, hit, tie);
+  }
+  if (k < end) {
+    const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+    double b0, d0;
+    if (CAM) {
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
+    } else {
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+    }
+    nearest_update(d0 > 0.0 ? isect_roots(b0, d0) : FARAWAY, (int)g0[RTX_G_IDX], tmin, hit, tie);
+  }
+}
+
+// Nearest hit through the culling tree: the always-tested spheres, then a stackless depth-first
+// walk that enters a node when any lane of the wave may hit it before its current nearest t.
+// Evaluation order differs from scene order, which the result does not depend on: the nearest t
+// is a minimum, `hit` is its unique owner unless tied, and a tie is flagged whatever the order.
+template <bool CAM>
+__device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double oy, double oz, double dx, double dy,
+                                            double dz, double& tmin, int& hit, bool& tie) {
+  const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
+  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
+  const int nn = (int)sc[RTX_H_NNODES];
+  const double oo = dot3(ox, oy, oz, ox, oy, oz);
+  tmin = FARAWAY;
+  hit = -1;
+  tie = false;
+  nearest_range<CAM>(cg, 0, (int)sc[RTX_H_NALWAYS], ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
+  int i = 0;
+  while (i < nn) {
+    const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
+    if (__ballot(node_may_hit(nd, ox, oy, oz, oo, dx, dy, dz, tmin)) != 0) {
+      const int cnt = (int)nd[RTX_N_COUNT];
+      if (cnt > 0) nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
+      ++i;
+    } else {
+      i = (int)nd[RTX_N_SKIP];
+    }
+  }
+}
+
+// Shadow any-hit through the culling tree (shader.py:126-128 in its any-hit form): lit stays true
+// unless some sphere is strictly nearer than the shape itself along the light direction.
+__device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
+                                        double ly, double lz, double tself) {
+  const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
+  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
+  const int nn = (int)sc[RTX_H_NNODES];
+  const int nal = (int)sc[RTX_H_NALWAYS];
+  bool lit = true;
+  for (int k = 0; k < nal; ++k) {
+    const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+    double b0, d0;
+    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+    if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
+  }
+  int i = 0;
+  while (i < nn) {
+    const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
+    if (__ballot(lit && node_may_hit(nd, qx, qy, qz, qq, lx, ly, lz, tself)) != 0) {
+      const int cnt = (int)nd[RTX_N_COUNT];
+      if (cnt > 0) {
+        const int first = (int)nd[RTX_N_FIRST], end = first + cnt;
+        int k = first;
+        for (; k + 1 < end; k += 2) {
+          const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+          const cdouble* g1 = g0 + RTX_GEOM_WORDS;
+          double b0, d0, b1, d1, t0, t1;
+          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+          isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
+          isect_pair_roots(b0, d0, b1, d1, t0, t1);
+          if (t0 < tself || t1 < tself) lit = false;
+        }
+        if (k < end) {
+          const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+          double b0, d0;
+          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+          if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
+        }
+      }
+      if (__ballot(lit) == 0) break;  // every lane of the wave is in shadow
+      ++i;
+    } else {
+      i = (int)nd[RTX_N_SKIP];
+    }
+  }
+  return lit;
+}
+
 // Nearest hit of ray (O, D) over all spheres; wave-uniform loop over sphere pairs, geometry through
 // the scalar cache. CAM: O is the camera (level 0), using the host-precomputed c.
-template <bool CAM>
-__device__ __forceinline__ void nearest_hit(const cdouble* geo, int nsph, double ox, double oy, double oz, double dx,
+template <bool CAM, typename P>
+__device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, double oy, double oz, double dx,
                                             double dy, double dz, double& tmin, int& hit, bool& tie) {
   tmin = FARAWAY;
   hit = -1;
@@ -239,8 +379,8 @@ __device__ __forceinline__ void nearest_hit(const cdouble* geo, int nsph, double
   const double oo = CAM ? 0.0 : dot3(ox, oy, oz, ox, oy, oz);
   int s = 0;
   for (; s + 1 < nsph; s += 2) {
-    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
-    const cdouble* g1 = g0 + RTX_GEOM_WORDS;
+    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const P* g1 = g0 + RTX_GEOM_WORDS;
     double b0, d0, b1, d1;
     if (CAM) {
       isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
@@ -255,7 +395,7 @@ __device__ __forceinline__ void nearest_hit(const cdouble* geo, int nsph, double
     nearest_update(t1, s + 1, tmin, hit, tie);
   }
   if (s < nsph) {
-    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
     double b0, d0;
     if (CAM) {
       isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
@@ -391,8 +531,8 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 // assembly (hit_color) and the reflection recursion (driven by the caller).
 // geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
 // same table (LDS copy or global).
-template <typename T>
-__device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, const T* tab, int nsph, int h, double ox,
+template <typename T, typename G>
+__device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* tab, int nsph, int h, double ox,
                                       double oy, double oz, double dx, double dy, double dz, double t, Hit& s) {
   const T* gh = tab + h * RTX_GEOM_WORDS;
   const T* mh = tab + nsph * RTX_GEOM_WORDS + h * RTX_MAT_WORDS;
@@ -403,6 +543,10 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
   const double nz = (pz - gh[RTX_G_CZ]) * inv_r;
   double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
   norm3(lx, ly, lz);  // :75
+#ifdef RTX_EARLY_V
+  double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
+  norm3(vx, vy, vz);  // :76 (interleaves with the L chain)
+#endif
   const double qx = px + nx * 0.0001, qy = py + ny * 0.0001, qz = pz + nz * 0.0001;  // :77
 
   // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
@@ -414,12 +558,14 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
   lit = tself > 1.0;
   const int nshadow = 0;
 #else
-  const int nshadow = nsph;
+  const bool culled = sc[RTX_H_NNODES] != 0.0;
+  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself);
+  const int nshadow = culled ? 0 : nsph;
 #endif
   int j = 0;
   for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
-    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
-    const cdouble* g1 = g0 + RTX_GEOM_WORDS;
+    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
+    const G* g1 = g0 + RTX_GEOM_WORDS;
     double b0, d0, b1, d1, t0, t1;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
     isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
@@ -430,7 +576,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
     }
   }
   if (lit && j < nshadow) {
-    const cdouble* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
+    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
     double b0, d0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
     if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
@@ -448,8 +594,10 @@ __device__ __forceinline__ void shade(const cdouble* sc, const cdouble* geo, con
   const bool need_irid = mh[RTX_M_IG] != 0.0;
   double spec = 0.0, va = 0.0;
   if (weighted || need_irid) {
+#ifndef RTX_EARLY_V
     double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
     norm3(vx, vy, vz);  // :76 (towards the camera on every level)
+#endif
 #ifdef RTX_ABL_SPEC  // timing ablation only (wrong output)
     if (weighted) spec = vx * lx + vy;
 #else
@@ -566,36 +714,66 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // k_render_fast<B, LDS>
 // ------------------------------------------------------------------------------------------
 
+// One block tile: (bx, by) in camera mode, block bx of 256 rays in explicit-ray mode. `first`: the
+// block's first tile, whose level-0 nearest-hit test overlaps the LDS staging of the scene table.
 template <int B, bool LDS>
-__global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p) {
+__device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
+#ifdef RTX_FIXED_S  // experiment: sphere count known at compile time (valid only for that scene)
+  const int nsph = RTX_FIXED_S;
+#else
   const int nsph = p.nsph;
-
-  extern __shared__ double lds_tab[];
-  if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block
-    const double* src = p.scene + RTX_HDR_WORDS;
-    for (int k = threadIdx.x; k < nsph * kSphWords; k += kBlock) lds_tab[k] = src[k];
-    __syncthreads();
-  }
+#endif
 
   int64_t i;
+  bool active;
   if (p.mode == 0) {
     // 2x2 waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = blockIdx.x * kTileW + (w & 1) * kWaveW + (lane % kWaveW);
-    const int lr = blockIdx.y * kTileH + (w >> 1) * kWaveH + (lane / kWaveW);
-    if (col >= p.width || lr >= p.n_rows) return;
+    const int col = bx * kTileW + (w & 1) * kWaveW + (lane % kWaveW);
+    const int lr = by * kTileH + (w >> 1) * kWaveH + (lane / kWaveW);
+    active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else {
-    i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= p.n) return;
+    i = (int64_t)bx * kBlock + threadIdx.x;
+    active = i < p.n;
   }
-  double ox, oy, oz, dx, dy, dz;
-  load_ray(p, i, ox, oy, oz, dx, dy, dz);
   const bool cam0 = (p.mode == 0);
+  #ifdef RTX_NOSTATS
+  unsigned long long* const st = nullptr;
+#else
   unsigned long long* st = p.stats;
-  if (st) stat_add(st, RTX_S_PIXELS, 1);
+#endif
+  double ox = 0.0, oy = 0.0, oz = 0.0, dx = 0.0, dy = 0.0, dz = 1.0;
+  // nearest hit of the current level's ray over all shapes (base.py:97-103): wave-uniform loop,
+  // geometry via s_load
+  double tmin = FARAWAY;
+  int hit = -1;
+  bool tie = false;
+  if (active) {
+    load_ray(p, i, ox, oy, oz, dx, dy, dz);
+    if (st) {
+      stat_add(st, RTX_S_PIXELS, 1);
+      stat_add(st, RTX_S_RAYS + 0, 1);
+      stat_wave(st, RTX_S_WTRACE + 0);
+    }
+    if (sc[RTX_H_NNODES] != 0.0) {
+      if (cam0) {
+        nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      } else {
+        nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      }
+    } else if (cam0) {
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+    } else {
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+    }
+  }
+  if constexpr (LDS) {
+    if (first) __syncthreads();
+  }
+  if (!active) return;
 
   // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level)
   constexpr int NS = B > 0 ? B : 1;
@@ -606,19 +784,6 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
   bool deferred = false;
 
   for (int k = 0;; ++k) {
-    if (st && k < RTX_S_LEVELS) {
-      stat_add(st, RTX_S_RAYS + k, 1);
-      stat_wave(st, RTX_S_WTRACE + k);
-    }
-    // nearest hit over all shapes (base.py:97-103), wave-uniform loop, geometry via s_load
-    double tmin;
-    int hit;
-    bool tie;
-    if (k == 0 && cam0) {
-      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
-    } else {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
-    }
     if (hit < 0) {  // nothing hit: NumpyRGBColor(0, 0, 0) (base.py:100)
       cr = cg = cb = 0.0;
       break;
@@ -634,7 +799,7 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
     }
     Hit s;
     if constexpr (LDS) {
-      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+      shade(sc, RTX_LOOP_GEO, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
     } else {
       shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
     }
@@ -659,6 +824,17 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
     ox = s.qx;
     oy = s.qy;
     oz = s.qz;
+    if (st && k + 1 < RTX_S_LEVELS) {
+      stat_add(st, RTX_S_RAYS + k + 1, 1);
+      stat_wave(st, RTX_S_WTRACE + k + 1);
+    }
+    if (sc[RTX_H_NNODES] != 0.0) {
+      nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+    } else if constexpr (LDS) {
+      nearest_hit<false>(RTX_LOOP_GEO, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+    } else {
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+    }
   }
 
   if (deferred) {
@@ -686,6 +862,25 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
     }
   }
   write_out(p, i, cr, cg, cb);
+}
+
+template <int B, bool LDS>
+__global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p) {
+  extern __shared__ double lds_tab[];
+  if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
+                        // in fast_tile, after the first tile's level-0 nearest-hit test)
+    const double* src = p.scene + RTX_HDR_WORDS;
+    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += kBlock) lds_tab[k] = src[k];
+  }
+  if (p.n_tiles_x == 0) {  // one tile per block
+    fast_tile<B, LDS>(p, blockIdx.x, blockIdx.y, true, lds_tab);
+    return;
+  }
+  // persistent blocks: tile t = (t % n_tiles_x, t / n_tiles_x), grid-stride
+  const int nt = p.n_tiles_x * p.n_tiles_y;
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    fast_tile<B, LDS>(p, t % p.n_tiles_x, t / p.n_tiles_x, t == (int)blockIdx.x, lds_tab);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -922,6 +1117,22 @@ inline void prof_next() {
   if (g_prof.cap && g_prof.used < g_prof.cap) ++g_prof.used;
 }
 
+#ifndef RTX_PERSIST_BLOCKS_PER_CU
+#define RTX_PERSIST_BLOCKS_PER_CU 0  // k_render_fast persistent blocks per CU (0: one block per tile)
+#endif
+
+int device_cus() {  // compute units of the current device (cached per device)
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
+
 int stack_levels_for(int max_bounces) {
   return max_bounces < 0 ? RTX_UNBOUNDED_LEVELS : max_bounces + 1;
 }
@@ -988,10 +1199,16 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack_levels = stack_levels_for(p.max_bounces);
   if (fast) {
     dim3 grid;
-    if (p.mode == 0) {
-      grid = dim3((p.width + kTileW - 1) / kTileW, (p.n_rows + kTileH - 1) / kTileH);
+    const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kBlock - 1) / kBlock);
+    const int ty = p.mode == 0 ? (p.n_rows + kTileH - 1) / kTileH : 1;
+    const int persist = RTX_PERSIST_BLOCKS_PER_CU * device_cus();
+    if (persist > 0 && (int64_t)tx * ty > persist) {
+      p.n_tiles_x = tx;
+      p.n_tiles_y = ty;
+      grid = dim3((unsigned)persist);
     } else {
-      grid = dim3((unsigned)((p.n + kBlock - 1) / kBlock));
+      p.n_tiles_x = p.n_tiles_y = 0;
+      grid = dim3((unsigned)tx, (unsigned)ty);
     }
     prof_mark(0, s);
     launch_fast(p.max_bounces, p, grid, s);

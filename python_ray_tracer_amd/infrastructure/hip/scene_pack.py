@@ -145,7 +145,72 @@ def pack_scene(scene) -> np.ndarray:
         m[L.M_REFL] = sh.reflection_gain
         m[L.M_IOR] = sh.specular_ior
         m[L.M_TFIOR] = sh.thin_film_ior
+    if S >= BVH_MIN_SPHERES:
+        blob = _append_culling_tree(blob, geo.copy(), S)
     return blob
+
+
+# --- culling hierarchy ----------------------------------------------------------------------
+# Scenes with many spheres get a bounding-sphere tree over the small spheres; huge spheres (the
+# R=99999 ground) are tested by every ray. The kernel's node test is conservative (margins far above
+# the reference formula's rounding error, rtx_kernels.hip node_may_hit), so culling changes no
+# result bit. The tree only reorders which spheres a ray examines.
+BVH_MIN_SPHERES = 8
+BVH_LEAF = 4
+HUGE_RADIUS = 100.0
+
+
+def _bound(centers: np.ndarray, radii: np.ndarray):
+    lo = (centers - radii[:, None]).min(axis=0)
+    hi = (centers + radii[:, None]).max(axis=0)
+    c = (lo + hi) * 0.5
+    R = float(np.max(np.sqrt(((centers - c) ** 2).sum(axis=1)) + radii))
+    R = R * (1 + 1e-12) + 1e-12  # absorb this computation's own rounding
+    return c, R
+
+
+def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarray:
+    centers = geo[:, L.G_CX:L.G_CZ + 1]
+    radii = np.sqrt(geo[:, L.G_RR])
+    huge = [i for i in range(S) if radii[i] > HUGE_RADIUS or float(np.abs(centers[i]).max()) > 1e4]
+    small = [i for i in range(S) if i not in set(huge)]
+    order = list(huge)
+    nodes = []
+
+    def rec(idx):
+        me = len(nodes)
+        nodes.append(None)
+        c, R = _bound(centers[idx], radii[idx])
+        if len(idx) <= BVH_LEAF:
+            first = len(order)
+            order.extend(sorted(idx))
+            rec_node = [c[0], c[1], c[2], R, first, len(idx), 0, 0.0]
+        else:
+            pts = centers[idx]
+            axis = int(np.argmax(pts.max(axis=0) - pts.min(axis=0)))
+            srt = sorted(idx, key=lambda i: (centers[i][axis], i))
+            half = len(srt) // 2
+            rec_node = [c[0], c[1], c[2], R, 0, 0, 0, 0.0]
+            nodes[me] = rec_node
+            rec(srt[:half])
+            rec(srt[half:])
+        rec_node[L.N_SKIP] = len(nodes)
+        rec_node[L.N_CC] = (float(np.sqrt((np.asarray(c) ** 2).sum())) + R) ** 2
+        nodes[me] = rec_node
+
+    if small:
+        rec(small)
+    node_arr = np.asarray(nodes, dtype=np.float64).reshape(-1, L.NODE_WORDS)
+    cgeo = geo[order].copy()
+    cgeo[:, L.G_IDX] = order
+    hdr_nodes = blob.size
+    hdr_cgeo = hdr_nodes + node_arr.size
+    out = np.concatenate([blob, node_arr.ravel(), cgeo.ravel()])
+    out[L.H_NNODES] = len(nodes)
+    out[L.H_NALWAYS] = len(huge)
+    out[L.H_NODES] = hdr_nodes
+    out[L.H_CGEO] = hdr_cgeo
+    return out
 
 
 def sphere_geometry(center, radius) -> np.ndarray:

@@ -94,6 +94,51 @@ def test_pack_matches_reference_expressions():
             assert np.array_equal(got, want), (W, H)
 
 
+@pytest.mark.parametrize("n", [0, 7, 8, 16, 64, 200])
+def test_culling_tree_invariants(n):
+    """Packer's bounding-sphere tree: every small sphere in exactly one leaf, leaves' bounds contain
+    their spheres (and every ancestor's bound contains them), skip links close each subtree, huge
+    spheres are in the always-tested prefix."""
+    spec = scenes.random_spec(n, 3, 64, 36)
+    blob = scene_pack.pack_scene(scenes.build_scene(spec))
+    S = n + 1
+    nn = int(blob[L.H_NNODES])
+    if S < scene_pack.BVH_MIN_SPHERES:
+        assert nn == 0
+        return
+    nodes = blob[int(blob[L.H_NODES]):int(blob[L.H_NODES]) + nn * L.NODE_WORDS].reshape(nn, L.NODE_WORDS)
+    cg = blob[int(blob[L.H_CGEO]):int(blob[L.H_CGEO]) + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
+    geo = blob[L.HDR_WORDS:L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
+    nal = int(blob[L.H_NALWAYS])
+    assert sorted(cg[:, L.G_IDX].astype(int).tolist()) == list(range(S))
+    assert nal == 1 and int(cg[0, L.G_IDX]) == n  # the ground sphere (appended last) is always tested
+    for k in range(S):  # the culled list carries the same geometry words
+        s = int(cg[k, L.G_IDX])
+        assert np.array_equal(cg[k, :L.G_IDX], geo[s, :L.G_IDX])
+    covered = []
+
+    def walk(i, ancestors):
+        node = nodes[i]
+        end = int(node[L.N_SKIP])
+        assert i < end <= nn
+        if node[L.N_COUNT] > 0:
+            for k in range(int(node[L.N_FIRST]), int(node[L.N_FIRST] + node[L.N_COUNT])):
+                covered.append(k)
+                s = int(cg[k, L.G_IDX])
+                for a in ancestors + [node]:
+                    assert np.linalg.norm(geo[s, :3] - a[:3]) + np.sqrt(geo[s, L.G_RR]) <= a[L.N_R]
+            assert end == i + 1
+            return end
+        j = i + 1
+        while j < end:
+            j = walk(j, ancestors + [node])
+        assert j == end
+        return end
+
+    assert walk(0, []) == nn
+    assert sorted(covered) == list(range(nal, S))
+
+
 def test_pack_error_behaviour():
     from python_ray_tracer_amd.domain import Camera, DomeLight, Scene3D
     from python_ray_tracer_amd.infrastructure.hip import HipRGBColor, HipVector3D
