@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--out", default="f32", choices=["f32", "f64", "u8"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0: skip)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
 
 
@@ -64,11 +66,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; --backend gloo (test mode) lets several ranks share fewer GPUs
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPUs")
+    local_dev = local % max(ndev, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
     spec, B = scenes.CONFIGS[args.config]()
     W, H = spec["camera"]["width"], spec["camera"]["height"]
@@ -92,7 +103,8 @@ def main():
                                             gather="u8" if args.out == "u8" else "color")
         px_per_step = W * H
 
-    def barrier():
+    def barrier():  # every rank's queued GPU work done, then all ranks meet
+        torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -108,8 +120,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms, kern_n = L.profile_collect()
     L.profile_enable(0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:  # the job takes as long as its slowest rank
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

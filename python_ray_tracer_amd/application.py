@@ -111,6 +111,8 @@ def render_frame_distributed(scene: Scene3D, render_service, *, group=None, row_
             pad = torch.zeros((tile.shape[0], (rmax - rows) * W), dtype=tile.dtype, device=tile.device)
             tile = torch.cat([tile, pad], 1)
     tile = tile.contiguous()
+    if dist.get_backend(group) == "gloo" and tile.is_cuda:  # gloo gathers host tensors
+        tile = tile.cpu()
     gathered = [torch.empty_like(tile) for _ in range(world)] if rank == dst else None
     dist.gather(tile, gathered, dst=dst, group=group)
     if rank != dst:
