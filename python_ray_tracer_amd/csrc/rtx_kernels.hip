@@ -52,12 +52,18 @@ constexpr int kTileH = 2 * kWaveH;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
-constexpr int kDeferredWorkers = 4096;  // general-kernel threads when it only serves ties
+#ifndef RTX_DEFERRED_WORKERS
+#define RTX_DEFERRED_WORKERS 4096
+#endif
+constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel threads when it only serves ties
 // geometry source of the wave-uniform sphere loops after level 0 (LDS variant: the LDS table)
 #ifdef RTX_GEO_LDS
 #define RTX_LOOP_GEO ((const double*)lds_tab)
 #else
 #define RTX_LOOP_GEO geo
+#endif
+#ifndef RTX_DIVERGENT_FAST
+#define RTX_UNIFORM_FAST 1  // sqrt/div fast path chosen per wave (ballot), not per lane (A/B: 1-2.5% faster)
 #endif
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
@@ -118,7 +124,12 @@ __device__ __forceinline__ double sqrt_core(double x) {  // x in [2^-767, DBL_MA
   return __builtin_fma(d, h, g);
 }
 __device__ __forceinline__ double sqrt_cr(double x) {
+#ifdef RTX_UNIFORM_FAST
+  // wave-uniform choice: the fast core unless some active lane is out of range
+  if (__ballot(!(x >= 0x1.0p-767 && x <= 0x1.fffffffffffffp+1023)) == 0) return sqrt_core(x);
+#else
   if (x >= 0x1.0p-767 && x <= 0x1.fffffffffffffp+1023) return sqrt_core(x);
+#endif
   return __builtin_sqrt(x);
 }
 // a / b for a, b with |.| in [2^-300, 2^300] (v_div_scale leaves them unchanged and clears VCC, so
@@ -138,7 +149,12 @@ __device__ __forceinline__ bool div_range(double x) {
   return ax >= 0x1.0p-300 && ax <= 0x1.0p+300;
 }
 __device__ __forceinline__ double div_cr(double a, double b) {
+#ifdef RTX_UNIFORM_FAST
+  if (__ballot(!(div_range(b) && (a == 0.0 || div_range(a)))) == 0)
+    return a == 0.0 ? a * __builtin_copysign(1.0, b) : div_core(a, b);
+#else
   if (div_range(b) && (a == 0.0 || div_range(a))) return a == 0.0 ? a * __builtin_copysign(1.0, b) : div_core(a, b);
+#endif
   return a / b;
 }
 
@@ -901,7 +917,8 @@ struct Stack {
   __device__ __forceinline__ double& at(int d, int f) const { return base[((int64_t)d * kFrameWords + f) * nw + w]; }
 };
 
-__device__ void trace_general(const Params& p, const Stack& S, double ox0, double oy0, double oz0, double dx0,
+template <typename Stk>
+__device__ void trace_general(const Params& p, const Stk& S, double ox0, double oy0, double oz0, double dx0,
                               double dy0, double dz0, double& cr, double& cg, double& cb) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;

@@ -68,22 +68,30 @@ def main():
             launch(k)
     torch.cuda.synchronize()
     times = [[] for _ in libs]
+    e2e = [[] for _ in libs]
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
         for k, lib in enumerate(libs):
             lib.rtx_profile_enable(a.iters)
+            ev0.record()
             for _ in range(a.iters):
                 launch(k)
+            ev1.record()
             ms = ctypes.c_double()
             cnt = ctypes.c_int()
             lib.rtx_profile_collect(ctypes.byref(ms), ctypes.byref(cnt))
             lib.rtx_profile_enable(0)
+            torch.cuda.synchronize()
             times[k].append(ms.value / max(cnt.value, 1) * 1e3)
+            e2e[k].append(ev0.elapsed_time(ev1) / a.iters * 1e3)
     torch.cuda.synchronize()
     for k, p in enumerate(a.libs):
         same = torch.equal(outs[k], outs[0])
         t = times[k]
         print(f"{Path(p).name:28s} median {statistics.median(t):9.2f} us  min {min(t):9.2f} us  "
-              f"Mpix/s(kernel) {n / statistics.median(t):10.1f}  equal_to_first={same}")
+              f"Mpix/s(kernel) {n / statistics.median(t):10.1f}  e2e/frame {statistics.median(e2e[k]):9.2f} us  "
+              f"equal_to_first={same}")
 
 
 if __name__ == "__main__":
