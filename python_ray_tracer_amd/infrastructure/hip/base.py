@@ -33,7 +33,7 @@ from python_ray_tracer_amd.application import Renderer
 from python_ray_tracer_amd.domain import Camera, RGBColor, Vector3D
 
 from . import _lib as L
-from .scene_pack import blob_key, camera_words, pack_scene
+from .scene_pack import camera_words, pack_key, scene_key
 
 FARAWAY = 1.0e39  # base.py:12
 
@@ -209,16 +209,17 @@ class HipRenderer(Renderer):
         return L.stream_handle(torch.cuda.current_stream(self.device))
 
     def scene_blob(self, scene) -> tuple[torch.Tensor, int]:
-        """Packed scene on the device (cached by content)."""
-        blob = pack_scene(scene)
-        key = blob_key(blob)
-        t = self._scene_cache.get(key)
-        if t is None:
-            t = torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True)
+        """Packed scene on the device, cached by content: the key is every value the render reads
+        from the scene (scene_pack.scene_key), so a mutated scene is re-packed and re-uploaded."""
+        key = scene_key(scene)
+        hit = self._scene_cache.get(key)
+        if hit is None:
+            blob = pack_key(*key)
+            hit = (torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True), int(blob[L.H_NSPH]))
             if len(self._scene_cache) >= 16:
                 self._scene_cache.pop(next(iter(self._scene_cache)))
-            self._scene_cache[key] = t
-        return t, int(blob[L.H_NSPH])
+            self._scene_cache[key] = hit
+        return hit
 
     def workspace(self, n: int) -> torch.Tensor:
         need = int(self._lib.rtx_workspace_bytes(int(n), self._bounces_arg))

@@ -13,6 +13,7 @@ renders unchanged.
 
 from __future__ import annotations
 
+import functools
 import hashlib
 
 import numpy as np
@@ -59,11 +60,25 @@ def _shape_fields(shape):
     pos = getattr(shape, "position", None) or getattr(shape, "center", None)
     if pos is None or not hasattr(shape, "radius") or not hasattr(shape, "shader"):
         raise TypeError(f"HipRenderer renders spheres only; got {type(shape).__name__}")
-    return _xyz(pos), shape.radius, shape.shader
+    sh = shape.shader
+    tex = sh.diffuse_color
+    if type(tex).__name__ == "TextureChecker":
+        tex_fields = (1.0, 1.0, 1.0, 1.0)
+    elif hasattr(tex, "color"):
+        tex_fields = (0.0,) + _xyz(tex.color)
+    else:
+        raise TypeError(f"unsupported texture {type(tex).__name__}")
+    # raw values, not float()-converted: the packer applies the reference's own expressions to them
+    return (_xyz(pos), shape.radius, tex_fields, sh.specular_gain, sh.diffuse_gain, sh.specular_roughness,
+            sh.specular_ior, sh.iridescence_gain, sh.thin_film_weight, sh.thin_film_thickness, sh.thin_film_ior,
+            sh.reflection_gain)
 
 
-def pack_scene(scene) -> np.ndarray:
-    """Flatten ``scene`` (shapes, lights, camera) into the float64 blob of include/rtx_hip.h."""
+def scene_key(scene) -> tuple:
+    """Everything a render reads from ``scene`` as a hashable pair
+    ``(static, camera)``: ``static`` = per-sphere geometry and material, lights[0].position and
+    the DomeLights; ``camera`` = (position, width, height). Raises what the reference raises for
+    an unrenderable scene (see pack_scene)."""
     shapes = list(scene.shapes)
     S = len(shapes)
     if S == 0:
@@ -74,80 +89,106 @@ def pack_scene(scene) -> np.ndarray:
     lights = list(scene.lights)
     light0 = lights[0]  # IndexError like shader.py:75 when the scene has no light
     lpos = light0.position  # AttributeError like shader.py:75 when lights[0] is a DomeLight
-    domes = [li for li in lights if type(li).__name__ == "DomeLight"]
+    domes = tuple((_xyz(d.color), float(d.intensity)) for d in lights if type(d).__name__ == "DomeLight")
     if len(domes) > L.MAX_DOMES:
         raise ValueError(f"at most {L.MAX_DOMES} DomeLights, got {len(domes)}")
     cam = scene.camera
-    cpos = _xyz(cam.position)
     W, H = int(cam.width), int(cam.height)
+    if W <= 0 or H <= 0:
+        raise ValueError(f"camera size must be positive, got {W}x{H}")
+    static = (tuple(_shape_fields(sh) for sh in shapes), _xyz(lpos), domes)
+    return static, (_xyz(cam.position), W, H)
 
+
+def pack_scene(scene) -> np.ndarray:
+    """Flatten ``scene`` (shapes, lights, camera) into the float64 blob of include/rtx_hip.h."""
+    static, camera = scene_key(scene)
+    return pack_key(static, camera)
+
+
+def pack_key(static: tuple, camera: tuple) -> np.ndarray:
+    """The blob of a ``scene_key`` pair: the camera-independent part is built once per distinct
+    ``static`` (cached), the camera words are applied to a copy."""
+    blob = _pack_static(static).copy()
+    _apply_camera(blob, *camera)
+    return blob
+
+
+@functools.lru_cache(maxsize=32)
+def _pack_static(static: tuple) -> np.ndarray:
+    spheres, lpos, domes = static
+    S = len(spheres)
     blob = np.zeros(L.HDR_WORDS + S * (L.GEOM_WORDS + L.MAT_WORDS), dtype=np.float64)
     h = blob[: L.HDR_WORDS]
     h[L.H_MAGIC] = L.MAGIC
     h[L.H_NSPH] = S
-    h[L.H_CAM:L.H_CAM + 3] = cpos
-    h[L.H_LIGHT:L.H_LIGHT + 3] = _xyz(lpos)
+    h[L.H_LIGHT:L.H_LIGHT + 3] = lpos
     dome_color = (1.0, 1.0, 1.0)  # shader.py:237
-    for i, d in enumerate(domes):
-        dome_color = _xyz(d.color)  # the last DomeLight's colour wins (shader.py:241)
-        h[L.H_DOMEI + i] = float(d.intensity)
+    for i, (color, intensity) in enumerate(domes):
+        dome_color = color  # the last DomeLight's colour wins (shader.py:241)
+        h[L.H_DOMEI + i] = intensity
     h[L.H_DOMEC:L.H_DOMEC + 3] = dome_color
     h[L.H_NDOME] = len(domes)
-    cw = camera_words(cpos, W, H)
-    h[L.H_XSTART], h[L.H_XSTEP], h[L.H_XSTOP], h[L.H_XFIX] = cw["xs"]
-    h[L.H_YSTART], h[L.H_YSTEP], h[L.H_YSTOP], h[L.H_YFIX] = cw["ys"]
-    h[L.H_VZ], h[L.H_VZ2] = cw["vz"], cw["vz2"]
-    h[L.H_W], h[L.H_H] = W, H
-    h[L.H_CAMOO] = cw["oo"]
-    ox, oy, oz = cpos
 
-    geo = blob[L.HDR_WORDS: L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
-    mat = blob[L.HDR_WORDS + S * L.GEOM_WORDS:].reshape(S, L.MAT_WORDS)
-    for s, shape in enumerate(shapes):
-        (cx, cy, cz), radius, sh = _shape_fields(shape)
+    geo_rows, mat_rows = [], []
+    for (cx, cy, cz), radius, tex, g, dg, rough, ior, ig, tfw, tft, tfior, refl in spheres:
         cc = (cx * cx + cy * cy) + cz * cz  # abs(self.position), shape.py:35
         rr = radius * radius  # shape.py:36
-        co = (cx * ox + cy * oy) + cz * oz
-        geo[s, L.G_CX:L.G_CZ + 1] = (cx, cy, cz)
-        geo[s, L.G_CC] = cc
-        geo[s, L.G_RR] = rr
-        geo[s, L.G_INVR] = 1.0 / radius  # shader.py:74
-        geo[s, L.G_C0] = ((cc + cw["oo"]) - 2 * co) - rr  # shape.py:35-37 with the camera origin
-
-        tex = sh.diffuse_color
-        m = mat[s]
-        m[L.M_G] = sh.specular_gain
-        m[L.M_DG] = sh.diffuse_gain
-        if type(tex).__name__ == "TextureChecker":
-            m[L.M_TEX] = 1.0
-            m[L.M_TR:L.M_TB + 1] = (1.0, 1.0, 1.0)
-        elif hasattr(tex, "color"):
-            m[L.M_TEX] = 0.0
-            m[L.M_TR:L.M_TB + 1] = _xyz(tex.color)
-        else:
-            raise TypeError(f"unsupported texture {type(tex).__name__}")
+        # G_C0 (camera-dependent) is filled by _apply_camera
+        geo_rows.append((cx, cy, cz, cc, rr, 1.0 / radius, 0.0, 0.0))  # 1/r: shader.py:74
+        m = [0.0] * L.MAT_WORDS
+        m[L.M_G] = g
+        m[L.M_DG] = dg
+        m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = tex
         # _calculate_physical_specular constants (shader.py:290-301), same Python expressions
-        alpha = sh.specular_roughness**2
-        F0 = ((sh.specular_ior - 1) / (sh.specular_ior + 1)) ** 2
+        alpha = rough**2
+        F0 = ((ior - 1) / (ior + 1)) ** 2
         m[L.M_A2] = alpha**2
         m[L.M_A2M1] = alpha**2 - 1
         m[L.M_1MA2] = 1 - alpha**2
         m[L.M_F0] = F0
         m[L.M_1MF0] = 1 - F0
         # _calculate_physical_iridescence constants (shader.py:208-232)
-        hue_shift = (sh.thin_film_ior - 1.0) / 2.0
-        m[L.M_IG] = sh.iridescence_gain
-        m[L.M_TFW] = sh.thin_film_weight
-        m[L.M_TFT] = sh.thin_film_thickness
+        hue_shift = (tfior - 1.0) / 2.0
+        m[L.M_IG] = ig
+        m[L.M_TFW] = tfw
+        m[L.M_TFT] = tft
         m[L.M_HS] = hue_shift
         m[L.M_1MHS] = 1.0 - hue_shift
-        m[L.M_ROUGH] = sh.specular_roughness
-        m[L.M_REFL] = sh.reflection_gain
-        m[L.M_IOR] = sh.specular_ior
-        m[L.M_TFIOR] = sh.thin_film_ior
+        m[L.M_ROUGH] = rough
+        m[L.M_REFL] = refl
+        m[L.M_IOR] = ior
+        m[L.M_TFIOR] = tfior
+        mat_rows.append(m)
+    geo = blob[L.HDR_WORDS: L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
+    geo[:] = np.asarray(geo_rows, dtype=np.float64)
+    blob[L.HDR_WORDS + S * L.GEOM_WORDS:] = np.asarray(mat_rows, dtype=np.float64).ravel()
     if S >= BVH_MIN_SPHERES:
         blob = _append_culling_tree(blob, geo.copy(), S)
+    blob.setflags(write=False)
     return blob
+
+
+def _apply_camera(blob: np.ndarray, cpos, W: int, H: int) -> None:
+    """Camera header words and every sphere's level-0 ``c`` (shape.py:35-37 with the camera as the
+    ray origin: ((|C|^2 + |O|^2) - 2 C.O) - r^2, elementwise in the reference's order)."""
+    h = blob[: L.HDR_WORDS]
+    cw = camera_words(cpos, W, H)
+    h[L.H_CAM:L.H_CAM + 3] = cpos
+    h[L.H_XSTART], h[L.H_XSTEP], h[L.H_XSTOP], h[L.H_XFIX] = cw["xs"]
+    h[L.H_YSTART], h[L.H_YSTEP], h[L.H_YSTOP], h[L.H_YFIX] = cw["ys"]
+    h[L.H_VZ], h[L.H_VZ2] = cw["vz"], cw["vz2"]
+    h[L.H_W], h[L.H_H] = W, H
+    h[L.H_CAMOO] = cw["oo"]
+    ox, oy, oz = cpos
+    S = int(h[L.H_NSPH])
+    tables = [blob[L.HDR_WORDS: L.HDR_WORDS + S * L.GEOM_WORDS]]
+    if h[L.H_NNODES]:
+        tables.append(blob[int(h[L.H_CGEO]): int(h[L.H_CGEO]) + S * L.GEOM_WORDS])
+    for t in tables:
+        geo = t.reshape(S, L.GEOM_WORDS)
+        co = (geo[:, L.G_CX] * ox + geo[:, L.G_CY] * oy) + geo[:, L.G_CZ] * oz
+        geo[:, L.G_C0] = ((geo[:, L.G_CC] + cw["oo"]) - 2 * co) - geo[:, L.G_RR]
 
 
 # --- culling hierarchy ----------------------------------------------------------------------
