@@ -337,9 +337,10 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
 }
 
 // Shadow any-hit through the culling tree (shader.py:126-128 in its any-hit form): lit stays true
-// unless some sphere is strictly nearer than the shape itself along the light direction.
+// unless some sphere is strictly nearer than the shape itself along the light direction. hs: the
+// wave-uniform shape of every lane (nsph when the lanes differ), whose own test cannot shadow it.
 __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
-                                        double ly, double lz, double tself) {
+                                        double ly, double lz, double tself, int hs) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
   const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
@@ -347,6 +348,7 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
   bool lit = true;
   for (int k = 0; k < nal; ++k) {
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+    if ((int)g0[RTX_G_IDX] == hs) continue;
     double b0, d0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
     if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
@@ -574,14 +576,20 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   lit = tself > 1.0;
   const int nshadow = 0;
 #else
+  // The shape's own test is t_self itself (same expression), and t_self < t_self never holds: when
+  // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
+  const int h0 = __builtin_amdgcn_readfirstlane(h);
+  const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
   const bool culled = sc[RTX_H_NNODES] != 0.0;
-  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself);
-  const int nshadow = culled ? 0 : nsph;
+  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs);
+  const int nshadow = culled ? 0 : nsph - (hs < nsph);
 #endif
   int j = 0;
   for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
-    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
-    const G* g1 = g0 + RTX_GEOM_WORDS;
+    const int j0 = __builtin_amdgcn_readfirstlane(j + (j >= hs));
+    const int j1 = __builtin_amdgcn_readfirstlane(j + 1 + (j + 1 >= hs));
+    const G* g0 = geo + j0 * RTX_GEOM_WORDS;
+    const G* g1 = geo + j1 * RTX_GEOM_WORDS;
     double b0, d0, b1, d1, t0, t1;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
     isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
@@ -592,7 +600,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
     }
   }
   if (lit && j < nshadow) {
-    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j) * RTX_GEOM_WORDS;
+    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
     double b0, d0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
     if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
@@ -1122,13 +1130,13 @@ struct Prof {
 } g_prof;
 
 void prof_free() {
-  for (int i = 0; i < 2 * g_prof.cap; ++i) hipEventDestroy(g_prof.ev[i]);
+  for (int i = 0; i < 2 * g_prof.cap; ++i) (void)hipEventDestroy(g_prof.ev[i]);
   delete[] g_prof.ev;
   g_prof = Prof{};
 }
 
 inline void prof_mark(int which, hipStream_t s) {
-  if (g_prof.cap && g_prof.used < g_prof.cap) hipEventRecord(g_prof.ev[2 * g_prof.used + which], s);
+  if (g_prof.cap && g_prof.used < g_prof.cap) (void)hipEventRecord(g_prof.ev[2 * g_prof.used + which], s);
 }
 inline void prof_next() {
   if (g_prof.cap && g_prof.used < g_prof.cap) ++g_prof.used;
