@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--mode", default="frames", choices=["frames", "tiles"])
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--out", default="f32", choices=["f32", "f64", "u8"])
+    ap.add_argument("--frames-per-step", type=int, default=1,
+                    help="frames mode: render this many orbit frames of the config (C5 camera path, "
+                         "SURVEY.md 8d) per step in ONE launch (rtx_render_frames)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0: skip)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -87,7 +90,16 @@ def main():
     dtype = torch.float64 if args.out == "f64" else torch.float32
     r = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev)
 
-    if args.mode == "frames":
+    F = max(1, args.frames_per_step)
+    if args.mode == "frames" and F > 1:
+        # rank r renders orbit frames r*F .. r*F+F-1 of a 256-frame orbit (C5 camera path)
+        batch = [scenes.build_scene(scenes.with_camera(spec, scenes.orbit_position(rank * F + f, 256)))
+                 for f in range(F)]
+
+        def step():
+            return r.render_batch(batch, out="u8" if args.out == "u8" else None)
+        px_per_step = W * H * F * world
+    elif args.mode == "frames":
         def step():
             if args.out == "u8":
                 return r.render_tile(scene, out="u8")
@@ -128,7 +140,10 @@ def main():
     # algorithmic work of one launch, from the kernel's own counters (checked against the oracle in
     # tests/test_gpu_parity.py): 15 flops / primary ray, 20 / ray-sphere test, 200 / shaded hit
     rs = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev, collect_stats=True)
-    if args.mode == "frames" or world == 1:
+    if args.mode == "frames" and F > 1:
+        rs.render_batch(batch)
+        n_px_launch = W * H * F
+    elif args.mode == "frames" or world == 1:
         rs.render_tile(scene)
         n_px_launch = W * H
     else:
@@ -141,7 +156,7 @@ def main():
     R_tr, R_sh = sum(st["rays"]), sum(st["hits"])
     flops = 15 * n_px_launch + 20 * S * (R_tr + R_sh) + 200 * R_sh
     out_bytes = {"f32": 12, "f64": 24, "u8": 3}[args.out]
-    alg_bytes = out_bytes * n_px_launch + 8 * len(r.scene_blob(scene)[0])  # framebuffer write + scene read
+    alg_bytes = out_bytes * n_px_launch + 8 * len(r.scene_blob(scene)[0]) * F  # framebuffer write + scene read
     kern_avg_s = kern_ms / 1e3 / max(kern_n, 1)
     achieved_tflops = flops / kern_avg_s / 1e12
     achieved_gbs = alg_bytes / kern_avg_s / 1e9
@@ -184,7 +199,7 @@ def main():
                 "C4": "64 random spheres + checker ground 7680x4320 seed 0",
                 "C5": "16 random spheres 1920x1080 seed 0"}[args.config] + f", {B} bounces",
                 "width": W, "height": H, "max_bounces": B, "spheres": S, "output": args.out,
-                "mode": args.mode, "parallelism": f"{args.mode}x{world}"},
+                "mode": args.mode, "frames_per_step": F, "parallelism": f"{args.mode}x{world}"},
             "roofline": {
                 "bound": "valu",
                 "kernel": f"k_render_fast<{B}>",

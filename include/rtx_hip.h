@@ -193,6 +193,17 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
                       int max_bounces, void* out, int out_kind,
                       void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
 
+/* Animation / batch driver (the reference renders one frame per
+ * render_image_pipeline call, application.py:43-52): n_frames whole frames of one size, sphere
+ * count and bounce cap in ONE launch. Frame f reads the blob at scenes + f * scene_stride (words;
+ * every blob is self-describing, so frames may differ in camera, spheres and lights) and writes
+ * its width*height pixels at out + f * (one frame's output bytes for out_kind). Equivalent to
+ * n_frames rtx_render_camera calls of whole frames. Workspace: rtx_workspace_bytes(n_frames *
+ * width * height, max_bounces). */
+int rtx_render_frames(const double* scenes, int64_t scene_stride, int n_frames, int n_spheres,
+                      int width, int height, int max_bounces, void* out, int out_kind,
+                      void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
+
 /* raytrace_scene(ray_origin, normalized_ray_direction, scene) for n rays (base.py:91-121),
  * including all reflection levels up to max_bounces. origins: [3][n] (origin_stride == n) or one
  * shared origin (origin_stride == 0, 3 doubles); dirs: [3][n]. */

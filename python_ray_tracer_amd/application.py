@@ -120,26 +120,52 @@ def render_frame_distributed(scene: Scene3D, render_service, *, group=None, row_
     return assemble(gathered, H, W, row_block, layout="hwc" if out == "u8" else "soa")
 
 
-def render_frames(frames, render_service, output_dir=None, *, group=None, name: str = "frame_{:04d}.png"):
+def render_frames(frames, render_service, output_dir=None, *, group=None, name: str = "frame_{:04d}.png",
+                  batch: int = 16):
     """Animation driver: ``frames`` is a sequence of Scene3D (one per frame). Frame k is rendered
     by rank k % world (no collective). Returns {k: colour} for this rank's frames; writes PNGs
-    when ``output_dir`` is given (skipping frames whose PNG already exists: resumable)."""
+    when ``output_dir`` is given (skipping frames whose PNG already exists: resumable).
+
+    With a renderer that has ``render_batch`` (HipRenderer), up to ``batch`` consecutive frames of
+    one camera size and sphere count go to the GPU in one launch (rtx_render_frames)."""
     dist = _dist_world(group)
     world = dist.get_world_size(group) if dist else 1
     rank = dist.get_rank(group) if dist else 0
-    out = {}
+    todo = []
     for k, scene in enumerate(frames):
         if k % world != rank:
             continue
         path = None if output_dir is None else Path(output_dir) / name.format(k)
         if path is not None and path.exists():
             continue
-        if hasattr(render_service, "render"):
-            color = render_service.render(scene)
+        todo.append((k, scene, path))
+    out = {}
+    batched = hasattr(render_service, "render_batch") and batch > 1
+    i = 0
+    while i < len(todo):
+        if batched:
+            shape = _frame_shape(todo[i][1])
+            j = i + 1
+            while j < len(todo) and j - i < batch and _frame_shape(todo[j][1]) == shape:
+                j += 1
+            colors = render_service.render_batch([sc for _, sc, _ in todo[i:j]])
+            chunk = [(k, sc, path, _color_of(colors[f])) for f, (k, sc, path) in enumerate(todo[i:j])]
         else:
-            dirs = render_service.get_ray_directions(scene.camera)
-            color = render_service.raytrace_scene(scene.camera.position, dirs, scene)
-        if path is not None:
-            render_service.save_image(color, scene.camera, path)
-        out[k] = color
+            k, scene, path = todo[i]
+            j = i + 1
+            if hasattr(render_service, "render"):
+                color = render_service.render(scene)
+            else:
+                dirs = render_service.get_ray_directions(scene.camera)
+                color = render_service.raytrace_scene(scene.camera.position, dirs, scene)
+            chunk = [(k, scene, path, color)]
+        for k, scene, path, color in chunk:
+            if path is not None:
+                render_service.save_image(color, scene.camera, path)
+            out[k] = color
+        i = j
     return out
+
+
+def _frame_shape(scene):
+    return int(scene.camera.width), int(scene.camera.height), len(list(scene.shapes))

@@ -59,6 +59,7 @@ EXPORTS = (
     "rtx_last_error",
     "rtx_workspace_bytes",
     "rtx_render_camera",
+    "rtx_render_frames",
     "rtx_trace_rays",
     "rtx_ray_directions",
     "rtx_sphere_intersect",
@@ -79,6 +80,8 @@ _SIGS = {
     "rtx_workspace_bytes": (_size, [_i64, _i32]),
     "rtx_render_camera": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
                                  _c_void_p, _size, _c_void_p, _c_void_p]),
+    "rtx_render_frames": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p, _size,
+                                 _c_void_p, _c_void_p]),
     "rtx_trace_rays": (_i32, [_c_void_p, _i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i32, _c_void_p,
                               _size, _c_void_p, _c_void_p]),
     "rtx_ray_directions": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),

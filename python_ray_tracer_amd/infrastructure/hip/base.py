@@ -290,6 +290,50 @@ class HipRenderer(Renderer):
         self._check_status(ws)
         return res
 
+    def render_batch(self, scenes, out: str | None = None) -> torch.Tensor:
+        """Whole frames of several scenes in ONE launch (rtx_render_frames).
+        All scenes need the same camera size and sphere count; cameras, spheres and lights may
+        differ (an animation). Returns [F, 3, W*H] colour (``out=None``) or [F, H, W, 3] uint8
+        (``out="u8"``); frame f equals ``render_tile(scenes[f], out=out)``."""
+        key, (blob, F, S, W, H) = self._batch_blob(scenes)
+        n = W * H
+        if out == "u8":
+            res = torch.empty((F, H, W, 3), dtype=torch.uint8, device=self.device)
+            kind = L.OUT_U8_HWC
+        else:
+            res = torch.empty((F, 3, n), dtype=self.color_dtype, device=self.device)
+            kind = _OUT_KIND[self.color_dtype]
+        ws = self.workspace(F * n)
+        L.check(self._lib.rtx_render_frames(blob.data_ptr(), blob.shape[1], F, S, W, H, self._bounces_arg,
+                                            res.data_ptr(), kind, ws.data_ptr(), ws.numel(), self._stats_ptr(),
+                                            self._stream()), "rtx_render_frames")
+        self._check_status(ws)
+        return res
+
+    def _batch_blob(self, scenes):
+        """[F, L] device array of packed scenes (padded to the longest blob), cached by content."""
+        keys = tuple(scene_key(sc) for sc in scenes)
+        if not keys:
+            raise ValueError("render_batch needs at least one scene")
+        ck = ("batch", keys)
+        hit = self._scene_cache.get(ck)
+        if hit is None:
+            (_, W, H) = keys[0][1]
+            S = len(keys[0][0][0])
+            for static, cam in keys:
+                if cam[1:] != (W, H) or len(static[0]) != S:
+                    raise ValueError("render_batch: every scene needs the same camera size and sphere count")
+            blobs = [pack_key(*k) for k in keys]
+            host = np.zeros((len(blobs), max(b.size for b in blobs)), dtype=np.float64)
+            for f, b in enumerate(blobs):
+                host[f, :b.size] = b
+            dev = torch.from_numpy(host).pin_memory().to(self.device, non_blocking=True)
+            hit = (dev, len(blobs), S, W, H)
+            if len(self._scene_cache) >= 16:
+                self._scene_cache.pop(next(iter(self._scene_cache)))
+            self._scene_cache[ck] = hit
+        return ck, hit
+
     def _trace(self, ray_origin, dirs, scene) -> torch.Tensor:
         blob, S = self.scene_blob(scene)
         D = _as_vector(dirs).to_tensor(self.device)

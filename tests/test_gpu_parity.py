@@ -123,6 +123,60 @@ def test_row_tiles_reassemble(hip):
         assert torch.equal(tiling.assemble(u8, 117, 200, rb, layout="hwc"), r.quantize(r.render(scene), scene.camera))
 
 
+def test_render_batch_matches_single_frames(hip):
+    """rtx_render_frames: an orbit animation (C5 camera path) and a batch of different scenes in
+    ONE launch equal one render per frame bit for bit, on the fast kernel (B=3) and beyond its cap
+    (B=10: the general kernel renders every ray of every frame)."""
+    base = scenes.random_spec(16, 0, 96, 54)
+    orbit = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 8))) for k in range(5)]
+    mixed = [scenes.build_scene(scenes.random_spec(16, seed, 96, 54)) for seed in (1, 2, 3)]
+    for B in (3, 10):
+        r = hip.HipRenderer(max_bounces=B)
+        for frames in (orbit, mixed):
+            batch = r.render_batch(frames)
+            assert batch.shape == (len(frames), 3, 96 * 54)
+            u8 = r.render_batch(frames, out="u8")
+            for f, sc in enumerate(frames):
+                assert torch.equal(batch[f], r.render_tile(sc)), (B, f)
+                assert torch.equal(u8[f], r.render_tile(sc, out="u8")), (B, f)
+    want = O.render(O.scene_from_spec(scenes.with_camera(base, scenes.orbit_position(3, 8))), 3)
+    got = hip.HipRenderer(max_bounces=3).render_batch(orbit)[3].cpu().numpy()
+    assert np.abs(got - want).max() <= ATOL
+    with pytest.raises(ValueError):
+        r.render_batch([orbit[0], scenes.build_scene(scenes.random_spec(15, 0, 96, 54))])
+
+
+def test_render_batch_ties_return_to_their_frame(hip, golden_meta, golden_renders):
+    """Deferred (tied) rays of a multi-frame launch carry their frame index to the general kernel."""
+    spec = golden_meta["cases"]["ties_64x36_B2"]["spec"]
+    cams = ([0, 0.2, -2], [0.3, 0.25, -2.5], [0, 0.2, -2], [-0.2, 0.1, -1.8])
+    frames = [scenes.build_scene(scenes.with_camera(spec, c)) for c in cams]
+    r = hip.HipRenderer(max_bounces=2, collect_stats=True)
+    batch = r.render_batch(frames)
+    assert r.stats()["deferred"] > 200
+    single = hip.HipRenderer(max_bounces=2)
+    for f, sc in enumerate(frames):
+        assert torch.equal(batch[f], single.render_tile(sc)), f
+    assert np.abs(batch[2].cpu().numpy() - golden_renders["ties_64x36_B2"]).max() <= ATOL
+
+
+def test_render_frames_driver_batches(hip, tmp_path):
+    """application.render_frames with a batching renderer: PNGs equal per-frame save_image output."""
+    from PIL import Image
+
+    from python_ray_tracer_amd.application import render_frames
+
+    base = scenes.random_spec(16, 0, 80, 45)
+    frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 6))) for k in range(6)]
+    r = hip.HipRenderer(max_bounces=3)
+    cols = render_frames(frames, r, tmp_path, batch=4)
+    assert sorted(cols) == list(range(6))
+    for k, sc in enumerate(frames):
+        ref = tmp_path / f"ref_{k}.png"
+        r.save_image(r.render(sc), sc.camera, ref)
+        assert np.array_equal(np.asarray(Image.open(tmp_path / f"frame_{k:04d}.png")), np.asarray(Image.open(ref)))
+
+
 def test_explicit_rays_and_intersect(hip, golden_meta):
     """rtx_trace_rays (raytrace_scene on arbitrary rays) and rtx_sphere_intersect (shape.py:28-51)."""
     spec = scenes.readme_spec(64, 36)
