@@ -47,8 +47,16 @@ constexpr int kBlock = 256;   // 4 waves
 #endif
 constexpr int kWaveW = RTX_WAVE_W;
 constexpr int kWaveH = 64 / kWaveW;
-constexpr int kTileW = 2 * kWaveW;  // block tile: 2 x 2 waves
-constexpr int kTileH = 2 * kWaveH;
+#ifndef RTX_BLOCK_WAVES
+#define RTX_BLOCK_WAVES 4  // waves per k_render_fast block (1, 2 or 4)
+#endif
+constexpr int kFastWaves = RTX_BLOCK_WAVES;
+static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "RTX_BLOCK_WAVES");
+constexpr int kFastBlock = 64 * kFastWaves;
+constexpr int kWavesX = kFastWaves == 1 ? 1 : 2;  // block tile: kWavesX x kWavesY waves
+constexpr int kWavesY = kFastWaves / kWavesX;
+constexpr int kTileW = kWavesX * kWaveW;
+constexpr int kTileH = kWavesY * kWaveH;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
@@ -773,18 +781,18 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   int64_t i;
   bool active;
   if (p.mode == 0) {
-    // 2x2 waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
+    // kWavesX x kWavesY waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = bx * kTileW + (w & 1) * kWaveW + (lane % kWaveW);
-    const int lr = by * kTileH + (w >> 1) * kWaveH + (lane / kWaveW);
+    const int col = bx * kTileW + (w % kWavesX) * kWaveW + (lane % kWaveW);
+    const int lr = by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else {
-    i = (int64_t)bx * kBlock + threadIdx.x;
+    i = (int64_t)bx * kFastBlock + threadIdx.x;
     active = i < p.n;
   }
   const bool cam0 = (p.mode == 0);
-  #ifdef RTX_NOSTATS
+#if defined(RTX_NOSTATS) || defined(RTX_WAVE_TIMES)  // RTX_WAVE_TIMES borrows the stats buffer
   unsigned long long* const st = nullptr;
 #else
   unsigned long long* st = p.stats;
@@ -909,14 +917,18 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 }
 
 template <int B, bool LDS>
-__global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p0) {
+__global__ __launch_bounds__(kFastBlock, RTX_FAST_WAVES) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
                         // in fast_tile, after the first tile's level-0 nearest-hit test)
     const double* src = p.scene + RTX_HDR_WORDS;
-    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += kBlock) lds_tab[k] = src[k];
+    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += kFastBlock) lds_tab[k] = src[k];
   }
+#ifdef RTX_WAVE_TIMES  // diagnostic (tools/wave_times.py): per-wave start/end, 100 MHz clock
+  const int64_t wslot = RTX_S_WORDS + 2 * ((((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * kFastWaves + (threadIdx.x >> 6));
+  if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (p.n_tiles_x == 0) {  // one tile per block
     // Bottom tile rows are dispatched first: they hold the ground and the spheres, whose pixels
     // run long bounce chains, while sky rows finish at level 0 and so fill the end of the grid
@@ -926,12 +938,17 @@ __global__ __launch_bounds__(kBlock, RTX_FAST_WAVES) void k_render_fast(Params p
 #else
     fast_tile<B, LDS>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 #endif
+#ifdef RTX_WAVE_TIMES
+    if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     return;
   }
-  // persistent blocks: tile t = (t % n_tiles_x, t / n_tiles_x), grid-stride
+  // several tiles per block: tile t of the bottom-up row-major order, grid-stride (block b renders
+  // tiles b, b + G, ...: a bottom-half tile, then a lighter upper one)
   const int nt = p.n_tiles_x * p.n_tiles_y;
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    fast_tile<B, LDS>(p, t % p.n_tiles_x, t / p.n_tiles_x, t == (int)blockIdx.x, lds_tab);
+    const int row = t / p.n_tiles_x;
+    fast_tile<B, LDS>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, t == (int)blockIdx.x, lds_tab);
   }
 }
 
@@ -1180,8 +1197,8 @@ inline void prof_next() {
   if (g_prof.cap && g_prof.used < g_prof.cap) ++g_prof.used;
 }
 
-#ifndef RTX_PERSIST_BLOCKS_PER_CU
-#define RTX_PERSIST_BLOCKS_PER_CU 0  // k_render_fast persistent blocks per CU (0: one block per tile)
+#ifndef RTX_TILES_PER_BLOCK
+#define RTX_TILES_PER_BLOCK 1  // k_render_fast tiles per block (grid-stride loop when > 1)
 #endif
 
 int device_cus() {  // compute units of the current device (cached per device)
@@ -1225,9 +1242,9 @@ template <int B>
 void launch_fast_b(const Params& p, dim3 grid, hipStream_t s) {
   if (p.nsph <= kLdsMaxSpheres) {
     const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double);
-    hipLaunchKernelGGL((k_render_fast<B, true>), grid, dim3(kBlock), lds, s, p);
+    hipLaunchKernelGGL((k_render_fast<B, true>), grid, dim3(kFastBlock), lds, s, p);
   } else {
-    hipLaunchKernelGGL((k_render_fast<B, false>), grid, dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((k_render_fast<B, false>), grid, dim3(kFastBlock), 0, s, p);
   }
 }
 
@@ -1266,13 +1283,13 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack_levels = stack_levels_for(p.max_bounces);
   if (fast) {
     dim3 grid;
-    const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kBlock - 1) / kBlock);
+    const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kFastBlock - 1) / kFastBlock);
     const int ty = p.mode == 0 ? (p.n_rows + kTileH - 1) / kTileH : 1;
-    const int persist = p.n_frames == 1 ? RTX_PERSIST_BLOCKS_PER_CU * device_cus() : 0;
-    if (persist > 0 && (int64_t)tx * ty > persist) {
+    const int64_t nt = (int64_t)tx * ty;
+    if (RTX_TILES_PER_BLOCK > 1 && nt > RTX_TILES_PER_BLOCK) {
       p.n_tiles_x = tx;
       p.n_tiles_y = ty;
-      grid = dim3((unsigned)persist);
+      grid = dim3((unsigned)((nt + RTX_TILES_PER_BLOCK - 1) / RTX_TILES_PER_BLOCK), 1, (unsigned)p.n_frames);
     } else {
       p.n_tiles_x = p.n_tiles_y = 0;
       grid = dim3((unsigned)tx, (unsigned)ty, (unsigned)p.n_frames);
