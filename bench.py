@@ -170,6 +170,8 @@ def main():
         except (ValueError, OSError):
             traffic = None
 
+    out_path = output_path_times(r, scene) if rank == 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(spec, B, args.cpu_seconds)
@@ -218,6 +220,7 @@ def main():
                         "FLOPs (SURVEY.md 8d model, kernel counters) / kernel time (HIP events, launch stream)",
             },
             "cpu_baseline": cpu,
+            "output_path": out_path,
         }
         if cpu:
             line["gpu_vs_cpu"] = round(value / cpu["value"], 1)
@@ -228,6 +231,35 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def output_path_times(r, scene):
+    """save_image's work for one frame, outside the timed step: device quantisation
+    to uint8 [H, W, 3], the D2H copy, and the PNG encode (best of 3 each)."""
+    import io
+
+    import torch
+
+    from python_ray_tracer_amd.infrastructure.hip.base import _write_png
+
+    color = r.render(scene)
+    q, d2h, png = [], [], []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        u8 = r.quantize(color, scene.camera)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        host = u8.cpu().numpy()
+        t2 = time.perf_counter()
+        _write_png(host, io.BytesIO())
+        t3 = time.perf_counter()
+        q.append(t1 - t0)
+        d2h.append(t2 - t1)
+        png.append(t3 - t2)
+    return {"quantize_ms": round(min(q) * 1e3, 4), "d2h_ms": round(min(d2h) * 1e3, 4),
+            "png_encode_ms": round(min(png) * 1e3, 3), "bytes": int(host.nbytes),
+            "note": "not in the timed step; PNG encode is PIL on one host core (base.py:143-151)"}
 
 
 def cpu_baseline(spec, B, budget_s):

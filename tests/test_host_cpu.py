@@ -194,3 +194,32 @@ def test_random_scene_generator_is_seeded():
         assert abs(s["center"][1] - (s["radius"] - 0.5)) < 1e-15
     sc = O.scene_from_spec(a)
     assert sc.spheres[-1].checker and sc.light_pos == (-2, 4, -1)
+
+
+def test_render_frames_batches_by_shape(tmp_path):
+    """application.render_frames: with a renderer that has render_batch, consecutive frames of one
+    camera size and sphere count go out in batches of at most `batch`; frames whose PNG exists are
+    skipped (resumable); every frame's colour comes back under its index."""
+    from python_ray_tracer_amd.application import render_frames
+
+    calls = []
+
+    class FakeBatchRenderer:
+        def render_batch(self, scenes_):
+            calls.append([int(s.camera.width) for s in scenes_])
+            return torch.stack([torch.full((3, int(s.camera.width) * int(s.camera.height)), float(len(s.shapes)))
+                                for s in scenes_])
+
+        def save_image(self, color, camera, path):
+            path.write_bytes(b"png")
+
+    def frame(w, n):
+        return scenes.build_scene(scenes.random_spec(n, 0, w, 4))
+
+    frames = [frame(8, 3), frame(8, 3), frame(8, 3), frame(6, 3), frame(6, 3), frame(8, 5), frame(8, 5)]
+    (tmp_path / "frame_0001.png").write_bytes(b"old")
+    out = render_frames(frames, FakeBatchRenderer(), tmp_path, batch=2)
+    assert sorted(out) == [0, 2, 3, 4, 5, 6]
+    assert calls == [[8, 8], [6, 6], [8, 8]]  # (0, 2), (3, 4), (5, 6): shape changes split batches
+    assert float(out[5].data[0, 0]) == 6.0  # 5 random spheres + ground
+    assert (tmp_path / "frame_0001.png").read_bytes() == b"old"
