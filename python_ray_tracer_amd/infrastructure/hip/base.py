@@ -432,4 +432,7 @@ def _write_png(hwc: np.ndarray, output_path) -> None:
 
     # base.py:145-151 builds three "L" images and merges them into "RGB": same pixels.
     img = Image.fromarray(np.ascontiguousarray(hwc, dtype=np.uint8))
-    img.save(output_path if hasattr(output_path, "write") else Path(output_path))
+    if hasattr(output_path, "write"):  # file object: PNG (a path's extension picks the format, like PIL in base.py:151)
+        img.save(output_path, format="PNG")
+    else:
+        img.save(Path(output_path))
