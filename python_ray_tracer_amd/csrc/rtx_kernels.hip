@@ -186,10 +186,20 @@ __device__ __forceinline__ double div_cr(double a, double b) {
   return a / b;
 }
 
+// 1.0 / where(mag == 0, 1, mag) with mag = sqrt(d), d = |v|^2 (NumpyVector3D.norm, base.py:61-64).
+// d in [2^-600, 2^600] puts sqrt's operand and the quotient's divisor (mag in [2^-300, 2^300],
+// non-zero) in both cores' exact ranges: one wave-uniform check instead of three.
+__device__ __forceinline__ double inv_mag(double d) {
+#ifdef RTX_UNIFORM_FAST
+  if (__ballot(!(d >= 0x1.0p-600 && d <= 0x1.0p+600)) == 0) return div_core(1.0, sqrt_core(d));
+#endif
+  const double mag = sqrt_cr(d);
+  return div_cr(1.0, mag == 0.0 ? 1.0 : mag);
+}
+
 __device__ __forceinline__ void norm3(double& x, double& y, double& z) {
   // NumpyVector3D.norm, base.py:61-64: v * (1.0 / where(mag == 0, 1, mag))
-  const double mag = sqrt_cr(dot3(x, y, z, x, y, z));
-  const double r = div_cr(1.0, mag == 0.0 ? 1.0 : mag);
+  const double r = inv_mag(dot3(x, y, z, x, y, z));
   x = x * r;
   y = y * r;
   z = z * r;
@@ -232,7 +242,7 @@ __device__ __forceinline__ double isect(const P* g, double ox, double oy, double
 }
 
 // The same test split in two halves so that two spheres' dependency chains interleave (and their
-// scalar loads share one wait): isect_disc computes b and the discriminant, isect_roots the rest.
+// scalar loads share one wait): isect_disc computes b and the discriminant, isect_sol the rest.
 template <typename P>
 __device__ __forceinline__ void isect_disc(const P* g, double ox, double oy, double oz, double oo, double dx,
                                            double dy, double dz, double& b, double& disc) {
@@ -248,36 +258,53 @@ __device__ __forceinline__ void isect_disc_cam(const P* g, double ox, double oy,
   b = 2.0 * dot3(dx, dy, dz, ox - g[RTX_G_CX], oy - g[RTX_G_CY], oz - g[RTX_G_CZ]);
   disc = (b * b) - (4.0 * g[RTX_G_C0]);
 }
-__device__ __forceinline__ double isect_roots(double b, double disc) {
-  // disc <= 0 lanes compute a dummy root (discarded below) so that every lane stays on sqrt_cr's
-  // fast path
-  const double sq = sqrt_cr(disc > 0.0 ? disc : 1.0);
-  const double s0 = (-b - sq) * 0.5;
+// The rest of the test, as a root and a validity flag instead of the FARAWAY sentinel (no f64
+// selects of a non-inline constant): valid <=> the reference returns the root, not FARAWAY. With
+// s0 <= s1 (rounding is monotone), (s0 > 0 ? s0 : s1) > 0 <=> s1 > 0. Lanes with disc <= 0 take
+// sqrt(|disc|), a discarded dummy that keeps them on sqrt_cr's fast path.
+__device__ __forceinline__ double isect_sol(double b, double disc, bool& valid) {
+  const double sq = sqrt_cr(fabs(disc));
+  const double s0 = (-b - sq) * 0.5;  // == / 2 exactly
   const double s1 = (-b + sq) * 0.5;
-  const double sol = s0 > 0.0 ? s0 : s1;  // see isect
-  return (disc > 0.0 && sol > 0.0) ? sol : FARAWAY;
+  valid = disc > 0.0 && s1 > 0.0;
+  return s0 > 0.0 ? s0 : s1;
+}
+// one sphere; the square root runs only if the discriminant is positive in some lane
+__device__ __forceinline__ double isect_one_sol(double b, double disc, bool& valid) {
+  valid = false;
+  double t = 0.0;
+  if (disc > 0.0) t = isect_sol(b, disc, valid);
+  return t;
 }
 // two spheres at once; the square roots run only if either discriminant is positive (per lane)
-__device__ __forceinline__ void isect_pair_roots(double b0, double disc0, double b1, double disc1, double& t0,
-                                                 double& t1) {
-  t0 = FARAWAY;
-  t1 = FARAWAY;
+__device__ __forceinline__ void isect_pair_sol(double b0, double disc0, double b1, double disc1, double& t0,
+                                               bool& v0, double& t1, bool& v1) {
+  v0 = v1 = false;
+  t0 = t1 = 0.0;
   if (disc0 > 0.0 || disc1 > 0.0) {
-    t0 = isect_roots(b0, disc0);
-    t1 = isect_roots(b1, disc1);
+    t0 = isect_sol(b0, disc0, v0);
+    t1 = isect_sol(b1, disc1, v1);
   }
 }
 
 // nearest-hit bookkeeping in scene order (base.py:97-103): the first strictly smaller t wins; an
-// equal t (not FARAWAY) marks a tie, which is cleared by any later strictly smaller t
-__device__ __forceinline__ void nearest_update(double t, int s, double& tmin, int& hit, bool& tie) {
-  if (t < tmin) {
+// equal t marks a tie, which is cleared by any later strictly smaller t. tmin starts at FARAWAY and
+// only decreases, so an invalid test (FARAWAY) never updates it. A valid root equal to FARAWAY
+// itself would flag a tie here: the pixel then goes to the general kernel, which is exact.
+__device__ __forceinline__ void nearest_update(bool valid, double t, int s, double& tmin, int& hit, bool& tie) {
+  if (valid && t < tmin) {
     tmin = t;
     hit = s;
     tie = false;
-  } else if (t == tmin && t != FARAWAY) {
+  } else if (valid && t == tmin) {
     tie = true;
   }
+}
+
+// Shadow any-hit: does test j (root t, validity v) come strictly before the shape's own distance
+// t_self? An invalid test is FARAWAY, which is before t_self only when t_self > FARAWAY (far_self).
+__device__ __forceinline__ bool shadows(bool valid, double t, double tself, bool far_self) {
+  return valid ? t < tself : far_self;
 }
 
 // ---- culling hierarchy ---------------------------------------------------------------------
@@ -320,9 +347,10 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
       isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
       isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1);
     }
-    isect_pair_roots(b0, d0, b1, d1, t0, t1);
-    nearest_update(t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
-    nearest_update(t1, (int)g1[RTX_G_IDX], tmin, hit, tie);
+    bool v0, v1;
+    isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+    nearest_update(v0, t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
+    nearest_update(v1, t1, (int)g1[RTX_G_IDX], tmin, hit, tie);
   }
   if (k < end) {
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
@@ -332,7 +360,9 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
     } else {
       isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
     }
-    nearest_update(d0 > 0.0 ? isect_roots(b0, d0) : FARAWAY, (int)g0[RTX_G_IDX], tmin, hit, tie);
+    bool v0;
+    const double t0 = isect_one_sol(b0, d0, v0);
+    nearest_update(v0, t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
   }
 }
 
@@ -367,6 +397,7 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
 // Shadow any-hit through the culling tree (shader.py:126-128 in its any-hit form): lit stays true
 // unless some sphere is strictly nearer than the shape itself along the light direction. hs: the
 // wave-uniform shape of every lane (nsph when the lanes differ), whose own test cannot shadow it.
+// Callers guarantee t_self <= FARAWAY in every lane (an invalid test then never shadows).
 __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
                                         double ly, double lz, double tself, int hs) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
@@ -379,7 +410,9 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
     if ((int)g0[RTX_G_IDX] == hs) continue;
     double b0, d0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
-    if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
+    bool v0;
+    const double t0 = isect_one_sol(b0, d0, v0);
+    if (v0 && t0 < tself) lit = false;
   }
   int i = 0;
   while (i < nn) {
@@ -395,14 +428,17 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
           double b0, d0, b1, d1, t0, t1;
           isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
           isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
-          isect_pair_roots(b0, d0, b1, d1, t0, t1);
-          if (t0 < tself || t1 < tself) lit = false;
+          bool v0, v1;
+          isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+          if ((v0 && t0 < tself) || (v1 && t1 < tself)) lit = false;
         }
         if (k < end) {
           const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
           double b0, d0;
           isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
-          if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
+          bool v0;
+          const double t0 = isect_one_sol(b0, d0, v0);
+          if (v0 && t0 < tself) lit = false;
         }
       }
       if (__ballot(lit) == 0) break;  // every lane of the wave is in shadow
@@ -436,9 +472,10 @@ __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, d
       isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1);
     }
     double t0, t1;
-    isect_pair_roots(b0, d0, b1, d1, t0, t1);
-    nearest_update(t0, s, tmin, hit, tie);
-    nearest_update(t1, s + 1, tmin, hit, tie);
+    bool v0, v1;
+    isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+    nearest_update(v0, t0, s, tmin, hit, tie);
+    nearest_update(v1, t1, s + 1, tmin, hit, tie);
   }
   if (s < nsph) {
     const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
@@ -448,7 +485,9 @@ __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, d
     } else {
       isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
     }
-    nearest_update(d0 > 0.0 ? isect_roots(b0, d0) : FARAWAY, s, tmin, hit, tie);
+    bool v0;
+    const double t0 = isect_one_sol(b0, d0, v0);
+    nearest_update(v0, t0, s, tmin, hit, tie);
   }
 }
 
@@ -600,15 +639,19 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   const double qq = dot3(qx, qy, qz, qx, qy, qz);
   const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
   bool lit = true;
-#ifdef RTX_ABL_SHADOW  // timing ablation only (wrong output)
-  lit = tself > 1.0;
-  const int nshadow = 0;
-#else
+  // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
+  // shadows. The linear loop handles it exactly; the culling tree skips missing spheres, so such
+  // a wave takes the linear loop.
+  const bool far_self = tself > FARAWAY;
   // The shape's own test is t_self itself (same expression), and t_self < t_self never holds: when
   // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
   const int h0 = __builtin_amdgcn_readfirstlane(h);
   const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
-  const bool culled = sc[RTX_H_NNODES] != 0.0;
+#ifdef RTX_ABL_SHADOW  // timing ablation only (wrong output)
+  lit = tself > 1.0;
+  const int nshadow = 0;
+#else
+  const bool culled = sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
   if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs);
   const int nshadow = culled ? 0 : nsph - (hs < nsph);
 #endif
@@ -621,8 +664,9 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
     double b0, d0, b1, d1, t0, t1;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
     isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
-    isect_pair_roots(b0, d0, b1, d1, t0, t1);
-    if (t0 < tself || t1 < tself) {
+    bool v0, v1;
+    isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+    if (shadows(v0, t0, tself, far_self) || shadows(v1, t1, tself, far_self)) {
       lit = false;
       break;
     }
@@ -631,7 +675,9 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
     const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
     double b0, d0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
-    if (d0 > 0.0 && isect_roots(b0, d0) < tself) lit = false;
+    bool v0;
+    const double t0 = isect_one_sol(b0, d0, v0);
+    if (shadows(v0, t0, tself, far_self)) lit = false;
   }
 
   const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));  // :138
@@ -698,8 +744,7 @@ __device__ __forceinline__ void camera_dir(const cdouble* sc, int col, int r, in
   const double vx = x - sc[RTX_H_CAM + 0];
   const double vy = y - sc[RTX_H_CAM + 1];
   const double vz = sc[RTX_H_VZ];
-  const double mag = sqrt_cr(((vx * vx) + (vy * vy)) + sc[RTX_H_VZ2]);
-  const double rr = div_cr(1.0, mag == 0.0 ? 1.0 : mag);
+  const double rr = inv_mag(((vx * vx) + (vy * vy)) + sc[RTX_H_VZ2]);
   dx = vx * rr;
   dy = vy * rr;
   dz = vz * rr;
