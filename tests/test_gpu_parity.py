@@ -260,3 +260,44 @@ def test_unbounded_recursion_limit(hip):
     scene = scenes.build_scene(spec)
     with pytest.raises(RecursionError):
         r.render(scene)
+
+
+def _fuzz_spec(seed):
+    """A harsher random scene than the bench generator: floating and overlapping spheres of mixed
+    sizes (some huge: always tested by the culling tree), a random light position, 0-2 domes, a
+    random camera (sometimes inside a sphere) and frame size."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([2, 5, 7, 8, 13, 24, 40]))
+    spec = scenes.random_spec(n, seed, int(rng.integers(9, 57)), int(rng.integers(7, 41)))
+    for sp in spec["spheres"][:-1]:
+        r = float(rng.choice([rng.uniform(0.02, 0.2), rng.uniform(0.2, 1.5), 150.0], p=[0.3, 0.65, 0.05]))
+        sp["radius"] = r
+        sp["center"] = [float(rng.uniform(-4, 4)), float(rng.uniform(-0.5, 3)), float(rng.uniform(0.5, 14))]
+        if r == 150.0:
+            sp["center"][2] += 200.0
+    spec["lights"][0]["position"] = [float(v) for v in rng.uniform([-6, 0.5, -6], [6, 8, 6])]
+    domes = int(rng.integers(0, 3))
+    spec["lights"] = spec["lights"][:1] + [{"kind": "dome", "intensity": float(rng.uniform(0, 0.3)),
+                                            "color": [float(v) for v in rng.uniform(0, 1, 3)]} for _ in range(domes)]
+    cam = [float(rng.uniform(-1.5, 1.5)), float(rng.uniform(-0.3, 1.5)), float(rng.uniform(-4, -0.5))]
+    if seed % 7 == 3:  # camera inside the first sphere
+        spec["spheres"][0]["center"] = [cam[0], cam[1], cam[2] + 0.1]
+        spec["spheres"][0]["radius"] = 0.8
+    spec["camera"]["position"] = cam
+    return spec
+
+
+@pytest.mark.parametrize("seed", range(14))
+def test_fuzz_scenes_against_oracle(hip, seed):
+    """Random scenes, cameras, sizes and bounce caps (both kernels; culled and linear sphere
+    loops): colour within ATOL, identical uint8, per-level ray/hit counts equal the oracle's."""
+    spec = _fuzz_spec(seed)
+    B = [0, 1, 2, 3, 5, 8, 9][seed % 7]
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL, (seed, np.abs(got - want).max())
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    assert np.array_equal(O.to_uint8(got, W, H), O.to_uint8(want, W, H))
+    s = r.stats()
+    assert s["rays"] == st.rays and s["hits"] == st.hits, seed

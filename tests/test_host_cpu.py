@@ -57,6 +57,11 @@ def test_workspace_bytes_and_error_paths():
     assert rc == -1 and b"null" in lib.rtx_last_error()
     rc = lib.rtx_render_camera(None, 3, 16, 16, 1, 2, 5, 16, 3, None, 0, None, 0, None, None)
     assert rc == -1 and b"geometry" in lib.rtx_last_error()
+    rc = lib.rtx_render_frames(None, 0, 2, 3, 16, 16, 3, None, 0, None, 0, None, None)
+    assert rc == -1 and b"scene_stride" in lib.rtx_last_error()
+    assert lib.rtx_render_frames(None, 64, -1, 3, 16, 16, 3, None, 0, None, 0, None, None) == -1
+    assert lib.rtx_render_frames(None, 64, 0, 3, 16, 16, 3, None, 0, None, 0, None, None) == 0  # nothing to do
+    assert lib.rtx_render_frames(None, 64, 70000, 3, 16, 16, 3, None, 0, None, 0, None, None) == -1
     assert lib.rtx_quantize_u8(None, 0, 10, None, None) == -1
     assert lib.rtx_sphere_intersect(None, None, 0, None, 5, None, None) == -1
 
