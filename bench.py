@@ -14,7 +14,8 @@ its interleaved row tile of ONE frame and the tiles are gathered to rank 0 (RCCL
 
 Timing: W untimed warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
 The dominant kernel's own time is measured live with HIP events recorded by the library on the
-launch stream (rtx_profile_*), for the roofline. Rank 0 also times the CPU oracle (NumPy float64,
+launch stream (rtx_profile_*) around one launch in --prof-every of the timed region, for the
+roofline (an event pair costs ~7 us of stream time, so timing every launch would depress `value`). Rank 0 also times the CPU oracle (NumPy float64,
 single core) on a bounded sample of the same workload.
 """
 
@@ -49,6 +50,9 @@ def parse():
                          "SURVEY.md 8d) per step in ONE launch (rtx_render_frames)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0: skip)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--prof-every", type=int, default=10,
+                    help="time the dominant kernel with HIP events on one launch in this many (an event pair "
+                         "adds ~7 us of stream time per launch; 1 = every launch)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -124,6 +128,7 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    L.profile_sample(max(1, args.prof_every))
     L.profile_enable(args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -132,6 +137,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms, kern_n = L.profile_collect()
     L.profile_enable(0)
+    L.profile_sample(1)
     if world > 1:  # the job takes as long as its slowest rank
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -211,13 +217,15 @@ def main():
                 "frac": round(achieved_tflops / PEAK_FP64_TFLOPS, 5),
                 "traffic": traffic,
                 "kernel_ms": round(kern_avg_s * 1e3, 5),
+                "kernel_launches_timed": kern_n,
                 "flops_per_launch": flops,
                 "rays_per_level": st["rays"],
                 "hits_per_level": st["hits"],
                 "hbm": {"achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "alg_bytes_per_launch": alg_bytes},
                 "note": "FP64 VALU-bound megakernel (no dense contraction, no MFMA); achieved = algorithmic "
-                        "FLOPs (SURVEY.md 8d model, kernel counters) / kernel time (HIP events, launch stream)",
+                        "FLOPs (SURVEY.md 8d model, kernel counters) / kernel time (HIP events on the launch "
+                        f"stream around 1 in {max(1, args.prof_every)} launches of the timed region)",
             },
             "cpu_baseline": cpu,
             "output_path": out_path,

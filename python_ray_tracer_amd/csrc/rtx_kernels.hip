@@ -1146,8 +1146,9 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0, int all_rays) 
   // (every block has read it before arriving; the next kernel on the stream sees the store)
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t prev = atomicAdd(hdr + RTX_WS_DONE, 1u);
-    if (prev == gridDim.x - 1) {
+    if (gridDim.x == 1) {  // one block: no other reader of the counter
+      hdr[RTX_WS_COUNT] = 0u;
+    } else if (atomicAdd(hdr + RTX_WS_DONE, 1u) == gridDim.x - 1) {
       hdr[RTX_WS_COUNT] = 0u;
       hdr[RTX_WS_DONE] = 0u;
     }
@@ -1227,19 +1228,26 @@ struct Prof {
   int cap = 0;
   int used = 0;
   hipEvent_t* ev = nullptr;  // 2 * cap
+  int every = 1;             // record one launch in `every` (rtx_profile_sample)
+  long long seen = 0;        // launches since rtx_profile_enable
+  bool on = false;           // the current launch is recorded
 } g_prof;
 
 void prof_free() {
   for (int i = 0; i < 2 * g_prof.cap; ++i) (void)hipEventDestroy(g_prof.ev[i]);
   delete[] g_prof.ev;
+  const int every = g_prof.every;
   g_prof = Prof{};
+  g_prof.every = every;
 }
 
 inline void prof_mark(int which, hipStream_t s) {
-  if (g_prof.cap && g_prof.used < g_prof.cap) (void)hipEventRecord(g_prof.ev[2 * g_prof.used + which], s);
+  if (which == 0) g_prof.on = g_prof.cap && g_prof.used < g_prof.cap && g_prof.seen++ % g_prof.every == 0;
+  if (g_prof.on) (void)hipEventRecord(g_prof.ev[2 * g_prof.used + which], s);
 }
 inline void prof_next() {
-  if (g_prof.cap && g_prof.used < g_prof.cap) ++g_prof.used;
+  if (g_prof.on) ++g_prof.used;
+  g_prof.on = false;
 }
 
 #ifndef RTX_TILES_PER_BLOCK
@@ -1385,6 +1393,12 @@ int rtx_profile_enable(int max_launches) {
     }
   }
   g_prof.cap = max_launches;
+  return RTX_OK;
+}
+
+int rtx_profile_sample(int every) {
+  if (every < 1) return fail(RTX_E_ARG, "profile sampling stride must be >= 1%s (%lld)", "", every);
+  g_prof.every = every;
   return RTX_OK;
 }
 

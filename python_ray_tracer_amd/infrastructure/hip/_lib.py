@@ -66,6 +66,7 @@ EXPORTS = (
     "rtx_quantize_u8",
     "rtx_profile_enable",
     "rtx_profile_collect",
+    "rtx_profile_sample",
     "rtx_selftest_math",
 )
 
@@ -89,6 +90,7 @@ _SIGS = {
     "rtx_quantize_u8": (_i32, [_c_void_p, _i32, _i64, _c_void_p, _c_void_p]),
     "rtx_profile_enable": (_i32, [_i32]),
     "rtx_profile_collect": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
+    "rtx_profile_sample": (_i32, [_i32]),
     "rtx_selftest_math": (_i32, [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
 }
 
@@ -130,6 +132,11 @@ def check(rc: int, what: str) -> None:
 
 def profile_enable(max_launches: int) -> None:
     check(load().rtx_profile_enable(int(max_launches)), "rtx_profile_enable")
+
+
+def profile_sample(every: int) -> None:
+    """Record one render launch in ``every`` while profiling is enabled (rtx_profile_sample)."""
+    check(load().rtx_profile_sample(int(every)), "rtx_profile_sample")
 
 
 def profile_collect() -> tuple[float, int]:

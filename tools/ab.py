@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--out", default="f32", choices=["f32", "f64", "u8"])
+    ap.add_argument("--no-events", action="store_true", help="end-to-end only: no per-launch kernel events")
     a = ap.parse_args()
     spec, B = scenes.CONFIGS[a.config]()
     scene = scenes.build_scene(spec)
@@ -73,7 +74,7 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
         for k, lib in enumerate(libs):
-            lib.rtx_profile_enable(a.iters)
+            lib.rtx_profile_enable(0 if a.no_events else a.iters)
             ev0.record()
             for _ in range(a.iters):
                 launch(k)
@@ -89,8 +90,9 @@ def main():
     for k, p in enumerate(a.libs):
         same = torch.equal(outs[k], outs[0])
         t = times[k]
-        print(f"{Path(p).name:28s} median {statistics.median(t):9.2f} us  min {min(t):9.2f} us  "
-              f"Mpix/s(kernel) {n / statistics.median(t):10.1f}  e2e/frame {statistics.median(e2e[k]):9.2f} us  "
+        km = statistics.median(t)
+        print(f"{Path(p).name:28s} median {km:9.2f} us  min {min(t):9.2f} us  "
+              f"Mpix/s(kernel) {n / km if km else float('nan'):10.1f}  e2e/frame {statistics.median(e2e[k]):9.2f} us  "
               f"equal_to_first={same}")
 
 
