@@ -65,14 +65,6 @@ constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this siz
 #endif
 constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel threads when it only serves ties
 // geometry source of the wave-uniform sphere loops after level 0 (LDS variant: the LDS table)
-#ifdef RTX_GEO_LDS
-#define RTX_LOOP_GEO ((const double*)lds_tab)
-#else
-#define RTX_LOOP_GEO geo
-#endif
-#ifndef RTX_DIVERGENT_FAST
-#define RTX_UNIFORM_FAST 1  // sqrt/div fast path chosen per wave (ballot), not per lane (A/B: 1-2.5% faster)
-#endif
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
 #endif
@@ -152,12 +144,8 @@ __device__ __forceinline__ double sqrt_core(double x) {  // x in [2^-767, DBL_MA
   return __builtin_fma(d, h, g);
 }
 __device__ __forceinline__ double sqrt_cr(double x) {
-#ifdef RTX_UNIFORM_FAST
-  // wave-uniform choice: the fast core unless some active lane is out of range
+  // wave-uniform choice (one ballot): the fast core unless some active lane is out of range
   if (__ballot(!(x >= 0x1.0p-767 && x <= 0x1.fffffffffffffp+1023)) == 0) return sqrt_core(x);
-#else
-  if (x >= 0x1.0p-767 && x <= 0x1.fffffffffffffp+1023) return sqrt_core(x);
-#endif
   return __builtin_sqrt(x);
 }
 // a / b for a, b with |.| in [2^-300, 2^300] (v_div_scale leaves them unchanged and clears VCC, so
@@ -177,12 +165,8 @@ __device__ __forceinline__ bool div_range(double x) {
   return ax >= 0x1.0p-300 && ax <= 0x1.0p+300;
 }
 __device__ __forceinline__ double div_cr(double a, double b) {
-#ifdef RTX_UNIFORM_FAST
-  if (__ballot(!(div_range(b) && (a == 0.0 || div_range(a)))) == 0)
+  if (__ballot(!(div_range(b) && (a == 0.0 || div_range(a)))) == 0)  // wave-uniform choice
     return a == 0.0 ? a * __builtin_copysign(1.0, b) : div_core(a, b);
-#else
-  if (div_range(b) && (a == 0.0 || div_range(a))) return a == 0.0 ? a * __builtin_copysign(1.0, b) : div_core(a, b);
-#endif
   return a / b;
 }
 
@@ -190,9 +174,7 @@ __device__ __forceinline__ double div_cr(double a, double b) {
 // d in [2^-600, 2^600] puts sqrt's operand and the quotient's divisor (mag in [2^-300, 2^300],
 // non-zero) in both cores' exact ranges: one wave-uniform check instead of three.
 __device__ __forceinline__ double inv_mag(double d) {
-#ifdef RTX_UNIFORM_FAST
   if (__ballot(!(d >= 0x1.0p-600 && d <= 0x1.0p+600)) == 0) return div_core(1.0, sqrt_core(d));
-#endif
   const double mag = sqrt_cr(d);
   return div_cr(1.0, mag == 0.0 ? 1.0 : mag);
 }
@@ -541,20 +523,6 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   return (NdotV <= 0.0) ? 0.0 : sf;  // :318
 }
 
-#ifdef RTX_IRID_CALL
-__device__ __attribute__((noinline)) void irid_terms(double va, double tft, double hs, double omhs, double w,
-                                                     double igain, double& ir, double& ig, double& ib) {
-  const double af = fabs(va - 0.5) * 2.0;  // :204
-  const double phase = ((af * RTX_PI) * tft) * 10.0;  // :208
-  const double ip = sin(phase);  // :211
-  const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
-  const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222
-  const double b = 0.5 + 0.5 * ip;  // :223
-  ir = (r * w) * igain;  // :229-232
-  ig = (gg * w) * igain;
-  ib = (b * w) * igain;
-}
-#endif
 
 // Colour of one shaded hit given the reflected colour R (shader.py:86-110):
 //   ((((0.004 + diffuse) + dome) + (spec + R*0.5)*g*lit) + irid)
@@ -586,11 +554,6 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   double ir = 0.0, ig = 0.0, ib = 0.0;
   const double igain = mh[RTX_M_IG];
   if (igain != 0.0) {
-#ifdef RTX_IRID_CALL
-    irid_terms(va, mh[RTX_M_TFT], mh[RTX_M_HS], mh[RTX_M_1MHS], mh[RTX_M_TFW], igain, ir, ig, ib);
-  }
-  if (false) {
-#endif
     const double af = fabs(va - 0.5) * 2.0;  // :204
     const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
 #ifdef RTX_ABL_SIN  // timing ablation only (wrong output)
@@ -628,10 +591,6 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   const double nz = (pz - gh[RTX_G_CZ]) * inv_r;
   double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
   norm3(lx, ly, lz);  // :75
-#ifdef RTX_EARLY_V
-  double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
-  norm3(vx, vy, vz);  // :76 (interleaves with the L chain)
-#endif
   const double qx = px + nx * 0.0001, qy = py + ny * 0.0001, qz = pz + nz * 0.0001;  // :77
 
   // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
@@ -692,10 +651,8 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   const bool need_irid = mh[RTX_M_IG] != 0.0;
   double spec = 0.0, va = 0.0;
   if (weighted || need_irid) {
-#ifndef RTX_EARLY_V
     double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
     norm3(vx, vy, vz);  // :76 (towards the camera on every level)
-#endif
 #ifdef RTX_ABL_SPEC  // timing ablation only (wrong output)
     if (weighted) spec = vx * lx + vy;
 #else
@@ -817,11 +774,7 @@ template <int B, bool LDS>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
-#ifdef RTX_FIXED_S  // experiment: sphere count known at compile time (valid only for that scene)
-  const int nsph = RTX_FIXED_S;
-#else
   const int nsph = p.nsph;
-#endif
 
   int64_t i;
   bool active;
@@ -837,7 +790,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     active = i < p.n;
   }
   const bool cam0 = (p.mode == 0);
-#if defined(RTX_NOSTATS) || defined(RTX_WAVE_TIMES)  // RTX_WAVE_TIMES borrows the stats buffer
+#ifdef RTX_WAVE_TIMES  // the wave-timing diagnostic borrows the stats buffer
   unsigned long long* const st = nullptr;
 #else
   unsigned long long* st = p.stats;
@@ -896,7 +849,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     Hit s;
     if constexpr (LDS) {
-      shade(sc, RTX_LOOP_GEO, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
     } else {
       shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
     }
@@ -928,7 +881,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (sc[RTX_H_NNODES] != 0.0) {
       nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
     } else if constexpr (LDS) {
-      nearest_hit<false>(RTX_LOOP_GEO, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
     } else {
       nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
     }
