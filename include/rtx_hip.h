@@ -94,18 +94,20 @@ enum {
   RTX_G_IDX = 7    /* scene index of the sphere (culled geometry list only)              */
 };
 
-/* culling-tree node words. A node bounds all spheres below it; the tree is stored depth-first
- * with a skip link, so a wave traverses it without a stack. A node is entered when any lane of
- * the wave may hit its bound (conservative test, see rtx_kernels.hip: a skipped sphere is one the
- * reference formula provably reports as FARAWAY); leaves list their spheres as a range of the
- * culled geometry list. */
+/* culling-tree node words. A node bounds all spheres below it with an axis-aligned box; the tree
+ * is stored depth-first with a skip link, so a wave traverses it without a stack. A node is
+ * entered when any lane's ray segment may meet the box expanded by the rounding margin of the
+ * reference formula (conservative test, see rtx_kernels.hip: a skipped sphere is one the reference
+ * formula provably reports as FARAWAY or beyond the current nearest distance); leaves list their
+ * spheres as a range of the culled geometry list. */
 enum {
-  RTX_NODE_WORDS = 8,
-  RTX_N_CX = 0, RTX_N_CY = 1, RTX_N_CZ = 2, RTX_N_R = 3,
-  RTX_N_FIRST = 4,  /* leaf: first culled-geometry entry   */
-  RTX_N_COUNT = 5,  /* leaf: sphere count (0: inner node)  */
-  RTX_N_SKIP = 6,   /* node index after this subtree        */
-  RTX_N_CC = 7      /* (|Cn| + R)^2, bounds |C|^2 of every sphere below (error budget) */
+  RTX_NODE_WORDS = 12,
+  RTX_N_LOX = 0, RTX_N_LOY = 1, RTX_N_LOZ = 2,  /* box minimum */
+  RTX_N_HIX = 3, RTX_N_HIY = 4, RTX_N_HIZ = 5,  /* box maximum */
+  RTX_N_FIRST = 6,  /* leaf: first culled-geometry entry   */
+  RTX_N_COUNT = 7,  /* leaf: sphere count (0: inner node)  */
+  RTX_N_SKIP = 8,   /* node index after this subtree        */
+  RTX_N_MARGIN = 9  /* 2e-7 * (3 (|Cn|+R)^2 + R^2 + 1), Cn/R: the box's bounding sphere (error budget) */
 };
 
 /* per-sphere material words (NumpyShader, shader.py:36-54; derived constants computed on the

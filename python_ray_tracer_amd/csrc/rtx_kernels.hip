@@ -290,25 +290,41 @@ __device__ __forceinline__ bool shadows(bool valid, double t, double tself, bool
 }
 
 // ---- culling hierarchy ---------------------------------------------------------------------
-// Conservative test: may any sphere inside the bound (centre Cn, radius R) produce, through the
-// reference formula (shape.py:34-51), a hit with 0 < t <= tlim? If this returns false, every such
-// sphere provably yields FARAWAY (or a t > tlim), so skipping it changes neither the nearest hit nor
-// the tie test nor the shadow test. Error budget: the reference's discriminant is computed with an
-// absolute error err <= ~64 eps * scale, scale = |Cn-O|^2 + (|Cn|+R)^2 + |O|^2 + R^2 (cancellation
-// in c = |C|^2 + |O|^2 - 2 C.O - r^2); through the square root a root moves by <= sqrt(err)
-// <= 1e-7 (scale + 1); the perpendicular distance by as much. Both margins below exceed that by a
-// wide factor, and |D| = 1 +- 1e-15 is absorbed too.
-__device__ __forceinline__ bool node_may_hit(const cdouble* nd, double ox, double oy, double oz, double oo, double dx,
-                                             double dy, double dz, double tlim) {
-  const double ocx = nd[RTX_N_CX] - ox, ocy = nd[RTX_N_CY] - oy, ocz = nd[RTX_N_CZ] - oz;
-  const double R = nd[RTX_N_R];
-  const double tca = dot3(ocx, ocy, ocz, dx, dy, dz);
-  const double oc2 = dot3(ocx, ocy, ocz, ocx, ocy, ocz);
-  const double scale = ((oc2 + nd[RTX_N_CC]) + oo) + R * R + 1.0;
-  const double lm = 1e-7 * scale;                      // distance margin
-  const double line = oc2 - tca * tca;                 // squared distance of Cn from the ray's line
-  const double rl = R + lm;
-  return line <= rl * rl && tca + R >= -lm && tca - R - lm <= tlim;
+// Conservative test: may any sphere inside a node's box produce, through the reference formula
+// (shape.py:34-51), a hit with 0 < t <= tlim? If this returns false, every such sphere provably
+// yields FARAWAY (or a t > tlim), so skipping it changes neither the nearest hit nor the tie test
+// nor the shadow test.
+// Error budget: the reference's discriminant carries an absolute error err <= ~64 eps * scale,
+// scale = |Cn-O|^2 + (|Cn|+R)^2 + |O|^2 + R^2 for a sphere inside the bounding sphere (Cn, R) of
+// the box (cancellation in c = |C|^2 + |O|^2 - 2 C.O - r^2). A root it reports is therefore within
+// sqrt(err) <= lm = 1e-7 (scale + 1) of a point of the sphere's ball, i.e. of the box expanded by
+// lm. With |Cn-O|^2 <= 2 (|Cn|+R)^2 + 2 |O|^2, lm <= 1e-7 (3 (|Cn|+R)^2 + R^2 + 1) + 3e-7 |O|^2; the
+// box is expanded by twice that (N_MARGIN + 6e-7 |O|^2), which also absorbs the slab arithmetic's
+// own rounding (~1e-15 relative) and |D| = 1 +- 1e-15.
+struct RaySlab {
+  double ix, iy, iz;  // 1 / direction component, components below 1e-200 in magnitude nudged to it
+  double mo;          // 6e-7 |O|^2
+};
+__device__ __forceinline__ double slab_inv(double d) {
+  // the reciprocal only places slab boundaries: rcp + one Newton step (~1e-16 relative) suffices;
+  // the nudge keeps 0 * inf out of the slab products (a shift of 1e-200 * t is far below lm)
+  const double dd = fabs(d) < 1e-200 ? __builtin_copysign(1e-200, d) : d;
+  const double r = __builtin_amdgcn_rcp(dd);
+  return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
+}
+__device__ __forceinline__ RaySlab ray_slab(double dx, double dy, double dz, double oo) {
+  return RaySlab{slab_inv(dx), slab_inv(dy), slab_inv(dz), 6e-7 * oo};
+}
+__device__ __forceinline__ bool node_may_hit(const cdouble* nd, double ox, double oy, double oz, const RaySlab& r,
+                                             double tlim) {
+  const double m = nd[RTX_N_MARGIN] + r.mo;
+  const double ax = ((nd[RTX_N_LOX] - m) - ox) * r.ix, bx = ((nd[RTX_N_HIX] + m) - ox) * r.ix;
+  const double ay = ((nd[RTX_N_LOY] - m) - oy) * r.iy, by = ((nd[RTX_N_HIY] + m) - oy) * r.iy;
+  const double az = ((nd[RTX_N_LOZ] - m) - oz) * r.iz, bz = ((nd[RTX_N_HIZ] + m) - oz) * r.iz;
+  // a NaN slab (non-finite origin) is dropped by fmin/fmax: unconstrained, hence conservative
+  const double tn = __builtin_fmax(__builtin_fmax(__builtin_fmin(ax, bx), __builtin_fmin(ay, by)), __builtin_fmin(az, bz));
+  const double tf = __builtin_fmin(__builtin_fmin(__builtin_fmax(ax, bx), __builtin_fmax(ay, by)), __builtin_fmax(az, bz));
+  return tn <= tf && tf >= 0.0 && tn <= tlim;
 }
 
 // Nearest hit over entries [first, first + cnt) of the culled geometry list (pairs, scalar loads).
@@ -363,10 +379,11 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
   hit = -1;
   tie = false;
   nearest_range<CAM>(cg, 0, (int)sc[RTX_H_NALWAYS], ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
+  const RaySlab rs = ray_slab(dx, dy, dz, oo);
   int i = 0;
   while (i < nn) {
     const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
-    if (__ballot(node_may_hit(nd, ox, oy, oz, oo, dx, dy, dz, tmin)) != 0) {
+    if (__ballot(node_may_hit(nd, ox, oy, oz, rs, tmin)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
       if (cnt > 0) nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
       ++i;
@@ -396,10 +413,11 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
     const double t0 = isect_one_sol(b0, d0, v0);
     if (v0 && t0 < tself) lit = false;
   }
+  const RaySlab rs = ray_slab(lx, ly, lz, qq);
   int i = 0;
   while (i < nn) {
     const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
-    if (__ballot(lit && node_may_hit(nd, qx, qy, qz, qq, lx, ly, lz, tself)) != 0) {
+    if (__ballot(lit && node_may_hit(nd, qx, qy, qz, rs, tself)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
       if (cnt > 0) {
         const int first = (int)nd[RTX_N_FIRST], end = first + cnt;

@@ -46,8 +46,8 @@ H_NNODES, H_NALWAYS, H_NODES, H_CGEO = 33, 34, 35, 36
 # geometry words
 G_CX, G_CY, G_CZ, G_CC, G_RR, G_INVR, G_C0, G_IDX = 0, 1, 2, 3, 4, 5, 6, 7
 # culling-tree node words
-NODE_WORDS = 8
-N_CX, N_CY, N_CZ, N_R, N_FIRST, N_COUNT, N_SKIP, N_CC = range(8)
+NODE_WORDS = 12
+N_LOX, N_LOY, N_LOZ, N_HIX, N_HIY, N_HIZ, N_FIRST, N_COUNT, N_SKIP, N_MARGIN = range(10)
 # material words
 (M_G, M_DG, M_TEX, M_TR, M_TG, M_TB, M_A2, M_A2M1, M_1MA2, M_F0, M_1MF0, M_IG, M_TFW, M_TFT, M_HS, M_1MHS,
  M_ROUGH, M_REFL, M_IOR, M_TFIOR) = range(20)

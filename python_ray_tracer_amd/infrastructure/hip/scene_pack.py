@@ -192,22 +192,44 @@ def _apply_camera(blob: np.ndarray, cpos, W: int, H: int) -> None:
 
 
 # --- culling hierarchy ----------------------------------------------------------------------
-# Scenes with many spheres get a bounding-sphere tree over the small spheres; huge spheres (the
-# R=99999 ground) are tested by every ray. The kernel's node test is conservative (margins far above
-# the reference formula's rounding error, rtx_kernels.hip node_may_hit), so culling changes no
-# result bit. The tree only reorders which spheres a ray examines.
+# Scenes with many spheres get a tree of axis-aligned boxes over the small spheres (surface-area
+# split, up to BVH_LEAF spheres per leaf); huge spheres (the R=99999 ground) are tested by every
+# ray. The kernel's node test is conservative (margins far above the reference formula's rounding
+# error, rtx_kernels.hip node_may_hit), so culling changes no result bit. The tree only reorders
+# which spheres a ray examines.
 BVH_MIN_SPHERES = 8
 BVH_LEAF = 4
 HUGE_RADIUS = 100.0
 
 
-def _bound(centers: np.ndarray, radii: np.ndarray):
+def _box(centers: np.ndarray, radii: np.ndarray):
     lo = (centers - radii[:, None]).min(axis=0)
     hi = (centers + radii[:, None]).max(axis=0)
-    c = (lo + hi) * 0.5
-    R = float(np.max(np.sqrt(((centers - c) ** 2).sum(axis=1)) + radii))
-    R = R * (1 + 1e-12) + 1e-12  # absorb this computation's own rounding
-    return c, R
+    pad = 1e-12 * (np.abs(lo) + np.abs(hi)) + 1e-300  # absorb this computation's own rounding
+    return lo - pad, hi + pad
+
+
+def _area(lo, hi):
+    e = np.maximum(hi - lo, 0.0)
+    return float(e[0] * e[1] + e[1] * e[2] + e[2] * e[0])
+
+
+def _sah_split(idx, centers, radii):
+    """Best surface-area split of sphere list `idx` (sorted along one axis, prefix/suffix boxes)."""
+    best = None
+    for axis in range(3):
+        order = sorted(idx, key=lambda i: (centers[i][axis], i))
+        n = len(order)
+        lo_c = centers[order] - radii[order][:, None]
+        hi_c = centers[order] + radii[order][:, None]
+        pre_lo, pre_hi = np.minimum.accumulate(lo_c), np.maximum.accumulate(hi_c)
+        suf_lo = np.minimum.accumulate(lo_c[::-1])[::-1]
+        suf_hi = np.maximum.accumulate(hi_c[::-1])[::-1]
+        for k in range(1, n):
+            cost = _area(pre_lo[k - 1], pre_hi[k - 1]) * k + _area(suf_lo[k], suf_hi[k]) * (n - k)
+            if best is None or cost < best[0]:
+                best = (cost, order[:k], order[k:])
+    return best[1], best[2]
 
 
 def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarray:
@@ -221,23 +243,23 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
     def rec(idx):
         me = len(nodes)
         nodes.append(None)
-        c, R = _bound(centers[idx], radii[idx])
+        lo, hi = _box(centers[idx], radii[idx])
+        c = (lo + hi) * 0.5
+        R = float(np.sqrt(((hi - lo) ** 2).sum())) * 0.5
+        R = R * (1 + 1e-12) + 1e-12
+        cc = (float(np.sqrt((c ** 2).sum())) + R) ** 2
+        node = [lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], 0, 0, 0, 2e-7 * (3.0 * cc + R * R + 1.0), 0.0, 0.0]
         if len(idx) <= BVH_LEAF:
-            first = len(order)
+            node[L.N_FIRST] = len(order)
+            node[L.N_COUNT] = len(idx)
             order.extend(sorted(idx))
-            rec_node = [c[0], c[1], c[2], R, first, len(idx), 0, 0.0]
         else:
-            pts = centers[idx]
-            axis = int(np.argmax(pts.max(axis=0) - pts.min(axis=0)))
-            srt = sorted(idx, key=lambda i: (centers[i][axis], i))
-            half = len(srt) // 2
-            rec_node = [c[0], c[1], c[2], R, 0, 0, 0, 0.0]
-            nodes[me] = rec_node
-            rec(srt[:half])
-            rec(srt[half:])
-        rec_node[L.N_SKIP] = len(nodes)
-        rec_node[L.N_CC] = (float(np.sqrt((np.asarray(c) ** 2).sum())) + R) ** 2
-        nodes[me] = rec_node
+            left, right = _sah_split(idx, centers, radii)
+            nodes[me] = node
+            rec(left)
+            rec(right)
+        node[L.N_SKIP] = len(nodes)
+        nodes[me] = node
 
     if small:
         rec(small)

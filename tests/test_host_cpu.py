@@ -101,9 +101,9 @@ def test_pack_matches_reference_expressions():
 
 @pytest.mark.parametrize("n", [0, 7, 8, 16, 64, 200])
 def test_culling_tree_invariants(n):
-    """Packer's bounding-sphere tree: every small sphere in exactly one leaf, leaves' bounds contain
-    their spheres (and every ancestor's bound contains them), skip links close each subtree, huge
-    spheres are in the always-tested prefix."""
+    """Packer's box tree: every small sphere in exactly one leaf, leaves' boxes contain their
+    spheres (and every ancestor's box contains them), skip links close each subtree, margins are
+    positive, huge spheres are in the always-tested prefix."""
     spec = scenes.random_spec(n, 3, 64, 36)
     blob = scene_pack.pack_scene(scenes.build_scene(spec))
     S = n + 1
@@ -130,8 +130,11 @@ def test_culling_tree_invariants(n):
             for k in range(int(node[L.N_FIRST]), int(node[L.N_FIRST] + node[L.N_COUNT])):
                 covered.append(k)
                 s = int(cg[k, L.G_IDX])
+                r = np.sqrt(geo[s, L.G_RR])
                 for a in ancestors + [node]:
-                    assert np.linalg.norm(geo[s, :3] - a[:3]) + np.sqrt(geo[s, L.G_RR]) <= a[L.N_R]
+                    assert np.all(a[L.N_LOX:L.N_LOZ + 1] <= geo[s, :3] - r)
+                    assert np.all(geo[s, :3] + r <= a[L.N_HIX:L.N_HIZ + 1])
+                    assert a[L.N_MARGIN] >= 2e-7
             assert end == i + 1
             return end
         j = i + 1
