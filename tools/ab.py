@@ -41,8 +41,13 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--out", default="f32", choices=["f32", "f64", "u8"])
     ap.add_argument("--no-events", action="store_true", help="end-to-end only: no per-launch kernel events")
+    ap.add_argument("--bvh-leaf", type=int, default=None, help="override scene_pack.BVH_LEAF (spheres per leaf)")
     a = ap.parse_args()
     spec, B = scenes.CONFIGS[a.config]()
+    if a.bvh_leaf is not None:
+        from python_ray_tracer_amd.infrastructure.hip import scene_pack
+
+        scene_pack.BVH_LEAF = a.bvh_leaf
     scene = scenes.build_scene(spec)
     blob_np = pack_scene(scene)
     dev = torch.device("cuda", 0)
