@@ -61,9 +61,9 @@ constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
 #ifndef RTX_DEFERRED_WORKERS
-#define RTX_DEFERRED_WORKERS 4096
+#define RTX_DEFERRED_WORKERS 16384  // general-kernel threads serving deferred rays (A/B: 4096, 16384, 65536)
 #endif
-constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel threads when it only serves ties
+constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel threads (deferred rays only)
 // geometry source of the wave-uniform sphere loops after level 0 (LDS variant: the LDS table)
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
@@ -100,9 +100,21 @@ struct Params {
   int64_t scene_stride;
   int n_frames;
   int frame;  // set per block / per deferred ray (kernel side)
+  // the cap exceeds the fast kernel's levels (max_bounces > RTX_FAST_MAX_BOUNCES or unbounded):
+  // k_render_fast defers a pixel whose reflection chain is still alive after its last level
+  int deep_defer;
 };
 
-constexpr int kFrameShift = 40;  // deferred-list entry: pixel | frame << kFrameShift
+// Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
+// (hits counted through level b) + 1 << 60. The general kernel re-renders the pixel from level 0
+// and skips the per-level counts the fast kernel already made (a, b = -1: none).
+constexpr int kFrameShift = 40;
+constexpr int kRaysShift = 56;
+constexpr int kHitsShift = 60;
+__device__ __forceinline__ uint64_t deferred_entry(int64_t i, int frame, int rays_through, int hits_through) {
+  return (uint64_t)i | ((uint64_t)frame << kFrameShift) | ((uint64_t)(rays_through + 1) << kRaysShift) |
+         ((uint64_t)(hits_through + 1) << kHitsShift);
+}
 
 __device__ __forceinline__ int64_t out_bytes_per_pixel(int kind) {
   return kind == RTX_OUT_F32_SOA ? 12 : kind == RTX_OUT_F64_SOA ? 24 : 3;
@@ -850,6 +862,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
   bool deferred = false;
+  int rays_through = 0, hits_through = -1;  // per-level counts already made for this pixel
 
   for (int k = 0;; ++k) {
     if (hit < 0) {  // nothing hit: NumpyRGBColor(0, 0, 0) (base.py:100)
@@ -858,6 +871,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     if (tie) {  // several shapes shaded and summed: the general kernel takes this ray
       deferred = true;
+      rays_through = k;
+      hits_through = k - 1;
       if (st) stat_add(st, RTX_S_TIES, 1);
       break;
     }
@@ -872,6 +887,12 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
     }
     const bool weighted = s.lit && s.g != 0.0;
+    if (weighted && k >= B && p.deep_defer) {  // the chain goes on beyond this kernel's levels
+      deferred = true;
+      rays_through = k;
+      hits_through = k;
+      break;
+    }
     if (!weighted || k >= B) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
       const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
@@ -909,7 +930,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     uint32_t* hdr = (uint32_t*)p.ws;
     const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
     if ((int64_t)slot < p.list_cap) {
-      ((int64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = i | ((int64_t)p.frame << kFrameShift);
+      ((uint64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = deferred_entry(i, p.frame, rays_through, hits_through);
     } else {
       atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
     }
@@ -986,9 +1007,11 @@ struct Stack {
   __device__ __forceinline__ double& at(int d, int f) const { return base[((int64_t)d * kFrameWords + f) * nw + w]; }
 };
 
+// rays_through / hits_through: per-level counts the fast kernel already made for this pixel
 template <typename Stk>
 __device__ void trace_general(const Params& p, const Stk& S, double ox0, double oy0, double oz0, double dx0,
-                              double dy0, double dz0, double& cr, double& cg, double& cb) {
+                              double dy0, double dz0, double& cr, double& cg, double& cb, int rays_through,
+                              int hits_through) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const double* tab = p.scene + RTX_HDR_WORDS;
@@ -1008,7 +1031,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     int next = (int)S.at(d, F_NEXT);
     double tmin;
     if (next < 0) {  // new ray: nearest distance (base.py:97-98)
-      if (st && d < RTX_S_LEVELS) stat_add(st, RTX_S_RAYS + d, 1);
+      if (st && d < RTX_S_LEVELS && d > rays_through) stat_add(st, RTX_S_RAYS + d, 1);
       tmin = FARAWAY;
       int nh = 0;
       for (int s = 0; s < nsph; ++s) {
@@ -1020,7 +1043,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
           ++nh;
         }
       }
-      if (st && nh > 1) stat_add(st, RTX_S_TIES, 1);
+      if (st && nh > 1 && d > rays_through) stat_add(st, RTX_S_TIES, 1);
       S.at(d, F_TMIN) = tmin;
       S.at(d, F_AR) = 0.0; S.at(d, F_AG) = 0.0; S.at(d, F_AB) = 0.0;  // NumpyRGBColor(0, 0, 0)
       next = 0;
@@ -1055,7 +1078,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       S.at(d, F_NEXT) = (double)(ph + 1);
       continue;
     }
-    if (st && d < RTX_S_LEVELS) stat_add(st, RTX_S_HITS + d, 1);
+    if (st && d < RTX_S_LEVELS && d > hits_through) stat_add(st, RTX_S_HITS + d, 1);
     Hit s;
     shade(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s);
     const bool weighted = s.lit && s.g != 0.0;
@@ -1096,20 +1119,23 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0, int all_rays) 
     Stack S{p.stack, p.n_workers, w};
     for (int64_t item = w; item < count; item += p.n_workers) {
       int64_t i, f;
+      int rays_through = -1, hits_through = -1;
       if (all_rays) {
         f = item / p.n;
         i = item - f * p.n;
       } else {
-        const int64_t e = list[item];
-        f = e >> kFrameShift;
-        i = e & ((int64_t(1) << kFrameShift) - 1);
+        const uint64_t e = (uint64_t)list[item];
+        i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
+        f = (int64_t)((e >> kFrameShift) & 0xFFFF);
+        rays_through = (int)((e >> kRaysShift) & 0xF) - 1;
+        hits_through = (int)((e >> kHitsShift) & 0xF) - 1;
       }
       const Params q = frame_view(p0, (int)f);
       double ox, oy, oz, dx, dy, dz;
       load_ray(q, i, ox, oy, oz, dx, dy, dz);
       if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
       double cr, cg, cb;
-      trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb);
+      trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through);
       write_out(q, i, cr, cg, cb);
     }
   }
@@ -1221,6 +1247,10 @@ inline void prof_next() {
   g_prof.on = false;
 }
 
+#ifndef RTX_DEEP_LEVELS
+#define RTX_DEEP_LEVELS 5  // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
+                           // 8-level instantiation spills, 3 defers too many pixels)
+#endif
 #ifndef RTX_TILES_PER_BLOCK
 #define RTX_TILES_PER_BLOCK 1  // k_render_fast tiles per block (grid-stride loop when > 1)
 #endif
@@ -1258,7 +1288,7 @@ int64_t workers_for(int64_t n, int max_bounces, bool deferred_only = false) {
 size_t list_bytes(int64_t n) { return (size_t)n * sizeof(int64_t); }
 
 size_t ws_bytes(int64_t n, int max_bounces) {
-  const size_t stack = (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
+  const size_t stack = (size_t)workers_for(n, max_bounces, true) * stack_levels_for(max_bounces) * kFrameWords * 8;
   return RTX_WS_HDR_BYTES + ((list_bytes(n) + 255) / 256) * 256 + stack;
 }
 
@@ -1302,10 +1332,13 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.ws = (uint8_t*)workspace;
   p.list_cap = n_all;
   p.stack = (double*)(p.ws + RTX_WS_HDR_BYTES + ((list_bytes(n_all) + 255) / 256) * 256);
-  const bool fast = p.max_bounces >= 0 && p.max_bounces <= RTX_FAST_MAX_BOUNCES;
-  p.n_workers = workers_for(n_all, p.max_bounces, fast);
+  // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
+  // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
+  const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_FAST_MAX_BOUNCES;
+  p.deep_defer = capped ? 0 : 1;
+  p.n_workers = workers_for(n_all, p.max_bounces, true);
   p.stack_levels = stack_levels_for(p.max_bounces);
-  if (fast) {
+  {
     dim3 grid;
     const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kFastBlock - 1) / kFastBlock);
     const int ty = p.mode == 0 ? (p.n_rows + kTileH - 1) / kTileH : 1;
@@ -1319,19 +1352,13 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
       grid = dim3((unsigned)tx, (unsigned)ty, (unsigned)p.n_frames);
     }
     prof_mark(0, s);
-    launch_fast(p.max_bounces, p, grid, s);
+    launch_fast(capped ? p.max_bounces : RTX_DEEP_LEVELS, p, grid, s);
     prof_mark(1, s);
     prof_next();
     if (int e = check_launch("k_render_fast")) return e;
-  } else {
-    prof_mark(0, s);
   }
-  // deferred rays (ties) — or every ray when the cap is beyond the fast kernel
-  hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p, fast ? 0 : 1);
-  if (!fast) {
-    prof_mark(1, s);
-    prof_next();
-  }
+  // deferred rays: ties, and chains longer than the fast kernel's levels
+  hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p, 0);
   return check_launch("k_render_general");
 }
 
