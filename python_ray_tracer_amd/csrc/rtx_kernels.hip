@@ -997,8 +997,8 @@ __global__ __launch_bounds__(kFastBlock, RTX_FAST_WAVES) void k_render_fast(Para
 // running colour sum over its hits (base.py:100-119), and the pending hit whose reflection is
 // being traced (its colour inputs).
 enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_TMIN, F_NEXT, F_AR, F_AG, F_AB,
-       F_DLI, F_DI, F_SPEC, F_VA, F_KEY };
-static_assert(F_KEY < kFrameWords, "frame layout");
+       F_DLI, F_DI, F_SPEC, F_VA, F_KEY, F_LEFT };  // F_LEFT: hits of this ray not yet shaded
+static_assert(F_LEFT < kFrameWords, "frame layout");
 
 struct Stack {
   double* base;
@@ -1028,35 +1028,39 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     const double ox = S.at(d, F_OX), oy = S.at(d, F_OY), oz = S.at(d, F_OZ);
     const double dx = S.at(d, F_DX), dy = S.at(d, F_DY), dz = S.at(d, F_DZ);
     const double oo = dot3(ox, oy, oz, ox, oy, oz);
-    int next = (int)S.at(d, F_NEXT);
+    const int next = (int)S.at(d, F_NEXT);
     double tmin;
-    if (next < 0) {  // new ray: nearest distance (base.py:97-98)
+    int left;   // hits of this ray not yet shaded, this one included
+    int h = nsph;  // the shape shaded now (nsph: the ray is done)
+    if (next < 0) {  // new ray: nearest distance (base.py:97-98) and its first shape in scene order
       if (st && d < RTX_S_LEVELS && d > rays_through) stat_add(st, RTX_S_RAYS + d, 1);
       tmin = FARAWAY;
-      int nh = 0;
+      int nh = 0, first = nsph;
       for (int s = 0; s < nsph; ++s) {
         const double t = isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
         if (t < tmin) {
           tmin = t;
           nh = 1;
+          first = s;
         } else if (t == tmin && t != FARAWAY) {
           ++nh;
         }
       }
       if (st && nh > 1 && d > rays_through) stat_add(st, RTX_S_TIES, 1);
+      left = tmin != FARAWAY ? nh : 0;  // (nearest != FARAWAY) & (t == nearest), base.py:102-103
       S.at(d, F_TMIN) = tmin;
+      S.at(d, F_LEFT) = (double)left;
       S.at(d, F_AR) = 0.0; S.at(d, F_AG) = 0.0; S.at(d, F_AB) = 0.0;  // NumpyRGBColor(0, 0, 0)
-      next = 0;
+      if (left > 0) h = first;
     } else {
       tmin = S.at(d, F_TMIN);
-    }
-    // next shape (scene order) with t == nearest (base.py:102-103)
-    int h = nsph;
-    if (tmin != FARAWAY) {
-      for (int s = next; s < nsph; ++s) {
-        if (isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz) == tmin) {
-          h = s;
-          break;
+      left = (int)S.at(d, F_LEFT);
+      if (left > 0) {  // a tie: the next shape (scene order) with t == nearest
+        for (int s = next; s < nsph; ++s) {
+          if (isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz) == tmin) {
+            h = s;
+            break;
+          }
         }
       }
     }
@@ -1076,6 +1080,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
       S.at(d, F_AB) = S.at(d, F_AB) + xb;
       S.at(d, F_NEXT) = (double)(ph + 1);
+      S.at(d, F_LEFT) = S.at(d, F_LEFT) - 1.0;
       continue;
     }
     if (st && d < RTX_S_LEVELS && d > hits_through) stat_add(st, RTX_S_HITS + d, 1);
@@ -1095,6 +1100,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
       S.at(d, F_AB) = S.at(d, F_AB) + xb;
       S.at(d, F_NEXT) = (double)(h + 1);
+      S.at(d, F_LEFT) = (double)(left - 1);
       continue;
     }
     S.at(d, F_DLI) = s.dli; S.at(d, F_DI) = s.di; S.at(d, F_SPEC) = s.spec; S.at(d, F_VA) = s.va;
@@ -1251,6 +1257,9 @@ inline void prof_next() {
 #define RTX_DEEP_LEVELS 5  // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
                            // 8-level instantiation spills, 3 defers too many pixels)
 #endif
+#ifndef RTX_CAPPED_MAX
+#define RTX_CAPPED_MAX RTX_FAST_MAX_BOUNCES  // caps rendered entirely by k_render_fast<cap>
+#endif
 #ifndef RTX_TILES_PER_BLOCK
 #define RTX_TILES_PER_BLOCK 1  // k_render_fast tiles per block (grid-stride loop when > 1)
 #endif
@@ -1334,7 +1343,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack = (double*)(p.ws + RTX_WS_HDR_BYTES + ((list_bytes(n_all) + 255) / 256) * 256);
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
-  const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_FAST_MAX_BOUNCES;
+  const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_CAPPED_MAX;
   p.deep_defer = capped ? 0 : 1;
   p.n_workers = workers_for(n_all, p.max_bounces, true);
   p.stack_levels = stack_levels_for(p.max_bounces);
