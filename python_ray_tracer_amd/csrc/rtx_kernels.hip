@@ -64,6 +64,9 @@ constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this siz
 #define RTX_DEFERRED_WORKERS 16384  // general-kernel threads serving deferred rays (A/B: 4096, 16384, 65536)
 #endif
 constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel threads (deferred rays only)
+// the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
+// spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
+constexpr int kGeneralTreeMin = 32;
 // geometry source of the wave-uniform sphere loops after level 0 (LDS variant: the LDS table)
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
@@ -398,6 +401,52 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
     if (__ballot(node_may_hit(nd, ox, oy, oz, rs, tmin)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
       if (cnt > 0) nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
+      ++i;
+    } else {
+      i = (int)nd[RTX_N_SKIP];
+    }
+  }
+}
+
+// The general kernel's nearest pass through the culling tree: the nearest distance, how many
+// shapes share it and the first of them in scene order (base.py:97-103). Traversal order does not
+// matter: the minimum is order-free, equal distances are all counted, and the smallest scene index
+// among them is kept. A sphere at exactly the current nearest distance is never culled (its box is
+// reached at t <= tlim).
+__device__ __forceinline__ void count_update(bool valid, double t, int s, double& tmin, int& nh, int& first) {
+  if (valid && t < tmin) {
+    tmin = t;
+    nh = 1;
+    first = s;
+  } else if (valid && t == tmin) {
+    ++nh;
+    first = s < first ? s : first;
+  }
+}
+__device__ __forceinline__ void nearest_count_bvh(const cdouble* sc, double ox, double oy, double oz, double oo,
+                                                  double dx, double dy, double dz, double& tmin, int& nh,
+                                                  int& first) {
+  const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
+  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
+  const int nn = (int)sc[RTX_H_NNODES];
+  auto range = [&](int k, int end) {
+    for (; k < end; ++k) {
+      const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
+      double b0, d0;
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+      bool v0;
+      const double t0 = isect_one_sol(b0, d0, v0);
+      count_update(v0, t0, (int)g0[RTX_G_IDX], tmin, nh, first);
+    }
+  };
+  range(0, (int)sc[RTX_H_NALWAYS]);
+  const RaySlab rs = ray_slab(dx, dy, dz, oo);
+  int i = 0;
+  while (i < nn) {
+    const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
+    if (__ballot(node_may_hit(nd, ox, oy, oz, rs, tmin)) != 0) {
+      const int cnt = (int)nd[RTX_N_COUNT];
+      if (cnt > 0) range((int)nd[RTX_N_FIRST], (int)nd[RTX_N_FIRST] + cnt);
       ++i;
     } else {
       i = (int)nd[RTX_N_SKIP];
@@ -1036,14 +1085,18 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       if (st && d < RTX_S_LEVELS && d > rays_through) stat_add(st, RTX_S_RAYS + d, 1);
       tmin = FARAWAY;
       int nh = 0, first = nsph;
-      for (int s = 0; s < nsph; ++s) {
-        const double t = isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
-        if (t < tmin) {
-          tmin = t;
-          nh = 1;
-          first = s;
-        } else if (t == tmin && t != FARAWAY) {
-          ++nh;
+      if (sc[RTX_H_NNODES] != 0.0 && nsph >= kGeneralTreeMin) {
+        nearest_count_bvh(sc, ox, oy, oz, oo, dx, dy, dz, tmin, nh, first);
+      } else {
+        for (int s = 0; s < nsph; ++s) {
+          const double t = isect(tab + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz);
+          if (t < tmin) {
+            tmin = t;
+            nh = 1;
+            first = s;
+          } else if (t == tmin && t != FARAWAY) {
+            ++nh;
+          }
         }
       }
       if (st && nh > 1 && d > rays_through) stat_add(st, RTX_S_TIES, 1);
@@ -1136,13 +1189,22 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0, int all_rays) 
         rays_through = (int)((e >> kRaysShift) & 0xF) - 1;
         hits_through = (int)((e >> kHitsShift) & 0xF) - 1;
       }
-      const Params q = frame_view(p0, (int)f);
-      double ox, oy, oz, dx, dy, dz;
-      load_ray(q, i, ox, oy, oz, dx, dy, dz);
-      if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
-      double cr, cg, cb;
-      trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through);
-      write_out(q, i, cr, cg, cb);
+      // The scene is read through the scalar cache (wave-uniform pointers) while a wave's lanes may
+      // hold rays of different frames of a multi-frame launch: lanes sharing the first active
+      // lane's frame run together, then the next frame (a waterfall over the wave's frames).
+      for (bool todo = true; todo;) {
+        const int f0 = __builtin_amdgcn_readfirstlane((int)f);
+        if ((int)f == f0) {
+          const Params q = frame_view(p0, f0);
+          double ox, oy, oz, dx, dy, dz;
+          load_ray(q, i, ox, oy, oz, dx, dy, dz);
+          if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
+          double cr, cg, cb;
+          trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through);
+          write_out(q, i, cr, cg, cb);
+          todo = false;
+        }
+      }
     }
   }
   // leave the workspace clean for the next call: the last block to finish zeroes the counter
