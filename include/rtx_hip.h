@@ -142,7 +142,9 @@ enum {
 
 #define RTX_UNBOUNDED (-1)       /* max_bounces: no cap, like the reference recursion */
 #define RTX_UNBOUNDED_LEVELS 333 /* ~ Python's recursion limit / 3 frames per level */
-#define RTX_FAST_MAX_BOUNCES 8   /* bounce caps served by the register-resident kernel */
+#define RTX_FAST_MAX_BOUNCES 8   /* bounce caps served entirely by the register-resident kernel; a
+                                    larger or no cap runs it for a few levels and defers the
+                                    pixels whose chain goes on to the depth-first kernel */
 
 /* stats buffer (uint64 words, accumulated with atomics; pass NULL to disable) */
 enum {
@@ -234,7 +236,7 @@ int rtx_selftest_math(const double* a, const double* b, int64_t n, double* out, 
 
 /* Live timing of the dominant render kernel (used by bench.py for the roofline): after
  * rtx_profile_enable(k), the next k render launches record a hipEvent pair on their stream around
- * k_render_fast (or k_render_general when it renders every ray). rtx_profile_collect waits for
+ * k_render_fast. rtx_profile_collect waits for
  * the recorded events and returns the summed kernel time and the launch count, then resets.
  * rtx_profile_enable(0) disables. Not thread-safe; meant for benchmarks, not for graph capture. */
 int rtx_profile_enable(int max_launches);

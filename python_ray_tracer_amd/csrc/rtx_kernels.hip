@@ -19,14 +19,16 @@
 //                         col_k = ((A_k + (spec_k + col_{k+1}*0.5)*g_k) + I_k)      (shader.py:106-110)
 //                     exactly. Sphere geometry is read by the wave-uniform loops through the scalar
 //                     cache (s_load); the per-lane hit-sphere/material records come from an LDS copy
-//                     of the scene table (LDS = S <= kLdsMaxSpheres). A ray that meets a tie (two
+//                     of the scene table (LDS = S <= kLdsMaxSpheres). Scenes of >= 8 spheres carry
+//                     a tree of boxes that the loops walk wave-uniformly (exact culling). Tile rows
+//                     are dispatched bottom-up (longest work first). A ray that meets a tie (two
 //                     shapes at the same nearest distance, base.py:103 — both get shaded and summed)
-//                     is appended to a deferred list.
+//                     or, under a cap above 8 or none, a chain longer than RTX_DEEP_LEVELS levels is
+//                     appended to a deferred list.
 //   k_render_general  Any bounce cap, ties included: an explicit depth-first walk of the ray tree
-//                     with per-worker frame stacks in the workspace (HBM). Serves the deferred
-//                     list of k_render_fast, and every ray when B > RTX_FAST_MAX_BOUNCES. Its last
-//                     block resets the list counter, so the workspace is left zeroed for the next
-//                     call (no per-frame memset).
+//                     with per-worker frame stacks in the workspace (HBM). Renders the deferred
+//                     list of k_render_fast from level 0. Its last block resets the list counter,
+//                     so the workspace is left zeroed for the next call (no per-frame memset).
 //   k_ray_dirs, k_intersect, k_quantize — the remaining boundary functions.
 #include <hip/hip_runtime.h>
 
@@ -41,7 +43,7 @@
 
 namespace {
 
-constexpr int kBlock = 256;   // 4 waves
+constexpr int kBlock = 256;   // threads per block of the elementwise boundary kernels
 #ifndef RTX_WAVE_W
 #define RTX_WAVE_W 8  // pixels per wave row: a wave renders an RTX_WAVE_W x (64 / RTX_WAVE_W) tile
 #endif
@@ -67,7 +69,6 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel thread
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
-// geometry source of the wave-uniform sphere loops after level 0 (LDS variant: the LDS table)
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
 #endif
@@ -1167,38 +1168,30 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
   }
 }
 
-__global__ __launch_bounds__(64) void k_render_general(Params p0, int all_rays) {
+__global__ __launch_bounds__(64) void k_render_general(Params p0) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const Params& p = p0;
   uint32_t* hdr = (uint32_t*)p.ws;
-  int64_t count = all_rays ? p.n * p.n_frames : (int64_t)hdr[RTX_WS_COUNT];
-  if (!all_rays && count > p.list_cap) count = p.list_cap;
+  int64_t count = (int64_t)hdr[RTX_WS_COUNT];
+  if (count > p.list_cap) count = p.list_cap;
   const int64_t* list = (const int64_t*)(p.ws + RTX_WS_HDR_BYTES);
   if (w < p.n_workers) {
     Stack S{p.stack, p.n_workers, w};
     for (int64_t item = w; item < count; item += p.n_workers) {
-      int64_t i, f;
-      int rays_through = -1, hits_through = -1;
-      if (all_rays) {
-        f = item / p.n;
-        i = item - f * p.n;
-      } else {
-        const uint64_t e = (uint64_t)list[item];
-        i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
-        f = (int64_t)((e >> kFrameShift) & 0xFFFF);
-        rays_through = (int)((e >> kRaysShift) & 0xF) - 1;
-        hits_through = (int)((e >> kHitsShift) & 0xF) - 1;
-      }
+      const uint64_t e = (uint64_t)list[item];
+      const int64_t i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
+      const int f = (int)((e >> kFrameShift) & 0xFFFF);
+      const int rays_through = (int)((e >> kRaysShift) & 0xF) - 1;
+      const int hits_through = (int)((e >> kHitsShift) & 0xF) - 1;
       // The scene is read through the scalar cache (wave-uniform pointers) while a wave's lanes may
       // hold rays of different frames of a multi-frame launch: lanes sharing the first active
       // lane's frame run together, then the next frame (a waterfall over the wave's frames).
       for (bool todo = true; todo;) {
-        const int f0 = __builtin_amdgcn_readfirstlane((int)f);
-        if ((int)f == f0) {
+        const int f0 = __builtin_amdgcn_readfirstlane(f);
+        if (f == f0) {
           const Params q = frame_view(p0, f0);
           double ox, oy, oz, dx, dy, dz;
           load_ray(q, i, ox, oy, oz, dx, dy, dz);
-          if (all_rays && p.stats) stat_add(p.stats, RTX_S_PIXELS, 1);
           double cr, cg, cb;
           trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through);
           write_out(q, i, cr, cg, cb);
@@ -1429,7 +1422,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     if (int e = check_launch("k_render_fast")) return e;
   }
   // deferred rays: ties, and chains longer than the fast kernel's levels
-  hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p, 0);
+  hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);
   return check_launch("k_render_general");
 }
 
