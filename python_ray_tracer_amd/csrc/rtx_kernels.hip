@@ -62,10 +62,16 @@ constexpr int kTileH = kWavesY * kWaveH;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
+// general-kernel threads: ties only (caps <= RTX_FAST_MAX_BOUNCES; an empty launch costs more with
+// more blocks), or ties and deep chains (A/B for unbounded renders: 4096, 16384, 65536)
 #ifndef RTX_DEFERRED_WORKERS
-#define RTX_DEFERRED_WORKERS 16384  // general-kernel threads serving deferred rays (A/B: 4096, 16384, 65536)
+#define RTX_DEFERRED_WORKERS 4096
 #endif
-constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;  // general-kernel threads (deferred rays only)
+#ifndef RTX_DEEP_WORKERS
+#define RTX_DEEP_WORKERS 16384
+#endif
+constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
+constexpr int kDeepWorkers = RTX_DEEP_WORKERS;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
@@ -1338,11 +1344,13 @@ int stack_levels_for(int max_bounces) {
 constexpr size_t kStackBudget = size_t(512) << 20;  // general-kernel frame stacks: <= 512 MiB
 constexpr int64_t kMaxWorkers = 65536;
 
-int64_t workers_for(int64_t n, int max_bounces, bool deferred_only = false) {
+int64_t workers_for(int64_t n, int max_bounces) {
   const size_t per = (size_t)stack_levels_for(max_bounces) * kFrameWords * sizeof(double);
   int64_t w = (int64_t)(kStackBudget / per);
   if (w > kMaxWorkers) w = kMaxWorkers;
-  if (deferred_only && w > kDeferredWorkers) w = kDeferredWorkers;
+  const bool capped = max_bounces >= 0 && max_bounces <= RTX_CAPPED_MAX;
+  const int64_t cap = capped ? kDeferredWorkers : kDeepWorkers;
+  if (w > cap) w = cap;
   const int64_t need = ((n + 63) / 64) * 64;
   if (w > need) w = need;
   w = (w / 64) * 64;
@@ -1352,7 +1360,7 @@ int64_t workers_for(int64_t n, int max_bounces, bool deferred_only = false) {
 size_t list_bytes(int64_t n) { return (size_t)n * sizeof(int64_t); }
 
 size_t ws_bytes(int64_t n, int max_bounces) {
-  const size_t stack = (size_t)workers_for(n, max_bounces, true) * stack_levels_for(max_bounces) * kFrameWords * 8;
+  const size_t stack = (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
   return RTX_WS_HDR_BYTES + ((list_bytes(n) + 255) / 256) * 256 + stack;
 }
 
@@ -1400,7 +1408,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
   const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_CAPPED_MAX;
   p.deep_defer = capped ? 0 : 1;
-  p.n_workers = workers_for(n_all, p.max_bounces, true);
+  p.n_workers = workers_for(n_all, p.max_bounces);
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
     dim3 grid;
