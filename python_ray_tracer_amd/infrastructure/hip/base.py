@@ -43,7 +43,12 @@ def _is_tensor(x) -> bool:
 
 
 def _sqrt(x):
-    return torch.sqrt(x) if _is_tensor(x) else np.sqrt(x)
+    # correctly rounded, like np.sqrt: torch's CPU sqrt is not (its SIMD path is off by up to 1 ulp)
+    if _is_tensor(x):
+        if x.device.type == "cpu":
+            return torch.from_numpy(np.sqrt(x.detach().numpy()))
+        return torch.sqrt(x)
+    return np.sqrt(x)
 
 
 def _where(c, a, b):

@@ -231,3 +231,39 @@ def test_render_frames_batches_by_shape(tmp_path):
     assert calls == [[8, 8], [6, 6], [8, 8]]  # (0, 2), (3, 4), (5, 6): shape changes split batches
     assert float(out[5].data[0, 0]) == 6.0  # 5 random spheres + ground
     assert (tmp_path / "frame_0001.png").read_bytes() == b"old"
+
+
+@pytest.mark.parametrize("backend", ["numpy", "torch"])
+def test_vector_algebra_matches_reference_expressions(backend):
+    """HipVector3D (reference NumpyVector3D, base.py:28-79): dot = (xx + yy) + zz, abs = squared
+    norm, norm = v * (1 / where(|v| == 0, 1, |v|)), extract = np.extract, place = scatter into
+    zeros; with NumPy or (CPU) torch components, bit for bit."""
+    from python_ray_tracer_amd.infrastructure.hip import HipVector3D
+
+    rng = np.random.default_rng(5)
+    a = rng.normal(size=(3, 33))
+    b = rng.normal(size=(3, 33))
+    a[:, 7] = 0.0  # a zero vector: norm keeps it zero
+    cond = rng.random(33) < 0.4
+    wrap = (lambda x: torch.from_numpy(x)) if backend == "torch" else (lambda x: x)
+    va, vb = HipVector3D(*map(wrap, a)), HipVector3D(*map(wrap, b))
+
+    def arr(x):
+        return x.numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+
+    dot = (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]
+    assert np.array_equal(arr(va.dot(vb)), dot)
+    assert np.array_equal(arr(abs(va)), (a[0] * a[0] + a[1] * a[1]) + a[2] * a[2])
+    for got, want in ((va * vb, a * b), (va * 2.5, a * 2.5), (va + vb, a + b), (va - vb, a - b), (-va, -a),
+                      (va / 3.0, a / 3.0)):
+        assert all(np.array_equal(arr(g), w) for g, w in zip(got.components(), want))
+    mag = np.sqrt((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2])
+    want = a * (1.0 / np.where(mag == 0, 1, mag))
+    assert all(np.array_equal(arr(g), w) for g, w in zip(va.norm().components(), want))
+    ex = va.extract(wrap(cond))
+    assert all(np.array_equal(arr(g), np.extract(cond, w)) for g, w in zip(ex.components(), a))
+    back = ex.place(wrap(cond))
+    for g, w in zip(back.components(), a):
+        z = np.zeros(33)
+        np.place(z, cond, np.extract(cond, w))
+        assert np.array_equal(arr(g), z)
