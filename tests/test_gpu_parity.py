@@ -301,3 +301,17 @@ def test_fuzz_scenes_against_oracle(hip, seed):
     assert np.array_equal(O.to_uint8(got, W, H), O.to_uint8(want, W, H))
     s = r.stats()
     assert s["rays"] == st.rays and s["hits"] == st.hits, seed
+
+
+def test_vector_algebra_on_device(hip):
+    """HipVector3D with device tensors (the reference's NumpyVector3D algebra, base.py:28-79) equals
+    the NumPy expressions bit for bit, norm's zero guard and sqrt included."""
+    rng = np.random.default_rng(9)
+    a = rng.normal(size=(3, 4097)) * rng.choice([1e-3, 1.0, 1e3], size=(1, 4097))
+    a[:, 11] = 0.0
+    v = hip.HipVector3D(*(torch.from_numpy(c).cuda() for c in a))
+    mag = np.sqrt((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2])
+    want = a * (1.0 / np.where(mag == 0, 1, mag))
+    got = [c.cpu().numpy() for c in v.norm().components()]
+    assert all(np.array_equal(g, w) for g, w in zip(got, want))
+    assert np.array_equal(abs(v).cpu().numpy(), (a[0] * a[0] + a[1] * a[1]) + a[2] * a[2])
