@@ -100,6 +100,8 @@ struct Params {
   int out_kind;
   uint8_t* ws;
   int64_t list_cap;
+  double* records;   // resume records of deep deferrals (list slot -> record), rec_cap of them
+  int64_t rec_cap;
   double* stack;
   int64_t n_workers;
   int stack_levels;
@@ -121,6 +123,16 @@ struct Params {
 constexpr int kFrameShift = 40;
 constexpr int kRaysShift = 56;
 constexpr int kHitsShift = 60;
+// Resume record of a pixel deferred for depth at level L = RTX_DEEP_LEVELS: the next level's ray
+// (origin, direction) and the colour inputs (dli, di, spec, va, key) of levels 0..L; the general
+// kernel continues the chain at level L + 1 instead of re-rendering it from level 0.
+#ifndef RTX_DEEP_LEVELS
+#define RTX_DEEP_LEVELS 5  // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
+                           // 8-level instantiation spills, 3 defers too many pixels)
+#endif
+constexpr int kRecLevelWords = 5;
+constexpr int kRecWords = 6 + kRecLevelWords * (RTX_DEEP_LEVELS + 1);
+constexpr int64_t kMaxRecords = int64_t(1) << 18;
 __device__ __forceinline__ uint64_t deferred_entry(int64_t i, int frame, int rays_through, int hits_through) {
   return (uint64_t)i | ((uint64_t)frame << kFrameShift) | ((uint64_t)(rays_through + 1) << kRaysShift) |
          ((uint64_t)(hits_through + 1) << kHitsShift);
@@ -917,7 +929,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   int sKey[NS];  // hit sphere | checker bit << 16
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
-  bool deferred = false;
+  bool deferred = false, appended = false;
   int rays_through = 0, hits_through = -1;  // per-level counts already made for this pixel
 
   for (int k = 0;; ++k) {
@@ -944,9 +956,33 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     const bool weighted = s.lit && s.g != 0.0;
     if (weighted && k >= B && p.deep_defer) {  // the chain goes on beyond this kernel's levels
+      // k == B here: levels 0..B-1 are in the shift register (slot j = level B-1-j), level B in s
       deferred = true;
-      rays_through = k;
-      hits_through = k;
+      appended = true;
+      rays_through = hits_through = B;
+      uint32_t* hdr = (uint32_t*)p.ws;
+      const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
+      if ((int64_t)slot < p.list_cap) {
+        ((uint64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = deferred_entry(i, p.frame, B, B);
+        if constexpr (B == RTX_DEEP_LEVELS) {
+          if ((int64_t)slot < p.rec_cap) {
+          double* rec = p.records + (int64_t)slot * kRecWords;
+          double rx = dx, ry = dy, rz = dz;
+          reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
+          rec[0] = s.qx; rec[1] = s.qy; rec[2] = s.qz;
+          rec[3] = rx; rec[4] = ry; rec[5] = rz;
+          double* lv = rec + 6 + kRecLevelWords * B;
+          lv[0] = s.dli; lv[1] = s.di; lv[2] = s.spec; lv[3] = s.va; lv[4] = (double)(hit | (s.chk ? 0x10000 : 0));
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            double* lj = rec + 6 + kRecLevelWords * (B - 1 - j);
+            lj[0] = sDli[j]; lj[1] = sDi[j]; lj[2] = sSpec[j]; lj[3] = sVa[j]; lj[4] = (double)sKey[j];
+          }
+          }
+        }
+      } else {
+        atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
+      }
       break;
     }
     if (!weighted || k >= B) {
@@ -983,12 +1019,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   }
 
   if (deferred) {
-    uint32_t* hdr = (uint32_t*)p.ws;
-    const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
-    if ((int64_t)slot < p.list_cap) {
-      ((uint64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = deferred_entry(i, p.frame, rays_through, hits_through);
-    } else {
-      atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
+    if (!appended) {  // a tie (deep deferrals were appended with their resume record)
+      uint32_t* hdr = (uint32_t*)p.ws;
+      const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
+      if ((int64_t)slot < p.list_cap) {
+        ((uint64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = deferred_entry(i, p.frame, rays_through, hits_through);
+      } else {
+        atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
+      }
     }
     if (st) stat_add(st, RTX_S_DEFERRED, 1);
     return;
@@ -1064,10 +1102,14 @@ struct Stack {
 };
 
 // rays_through / hits_through: per-level counts the fast kernel already made for this pixel
+// rec: a resume record (deep deferral) or null. With a record, frames 0..L hold the levels the fast
+// kernel shaded, each with its single hit pending (its colour inputs, nothing accumulated yet), and
+// the walk starts with the level L + 1 ray; their fold below is the fast kernel's fold, instruction
+// for instruction (hit_color with lit and weighted set).
 template <typename Stk>
 __device__ void trace_general(const Params& p, const Stk& S, double ox0, double oy0, double oz0, double dx0,
                               double dy0, double dz0, double& cr, double& cg, double& cb, int rays_through,
-                              int hits_through) {
+                              int hits_through, const double* rec = nullptr) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const double* tab = p.scene + RTX_HDR_WORDS;
@@ -1076,10 +1118,24 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
   const int B = p.max_bounces;  // < 0: unbounded (bounded by the stack depth)
   unsigned long long* st = p.stats;
 
-  S.at(0, F_OX) = ox0; S.at(0, F_OY) = oy0; S.at(0, F_OZ) = oz0;
-  S.at(0, F_DX) = dx0; S.at(0, F_DY) = dy0; S.at(0, F_DZ) = dz0;
-  S.at(0, F_NEXT) = -1.0;
   int d = 0;
+  if (rec) {
+    const int L = rays_through;
+    for (int l = 0; l <= L; ++l) {
+      const double* lv = rec + 6 + kRecLevelWords * l;
+      S.at(l, F_DLI) = lv[0]; S.at(l, F_DI) = lv[1]; S.at(l, F_SPEC) = lv[2]; S.at(l, F_VA) = lv[3];
+      S.at(l, F_KEY) = lv[4];
+      S.at(l, F_AR) = 0.0; S.at(l, F_AG) = 0.0; S.at(l, F_AB) = 0.0;
+      S.at(l, F_NEXT) = (double)(((int)lv[4] & 0xFFFF) + 1);
+      S.at(l, F_LEFT) = 1.0;
+    }
+    d = L + 1;
+    ox0 = rec[0]; oy0 = rec[1]; oz0 = rec[2];
+    dx0 = rec[3]; dy0 = rec[4]; dz0 = rec[5];
+  }
+  S.at(d, F_OX) = ox0; S.at(d, F_OY) = oy0; S.at(d, F_OZ) = oz0;
+  S.at(d, F_DX) = dx0; S.at(d, F_DY) = dy0; S.at(d, F_DZ) = dz0;
+  S.at(d, F_NEXT) = -1.0;
   for (;;) {
     const double ox = S.at(d, F_OX), oy = S.at(d, F_OY), oz = S.at(d, F_OZ);
     const double dx = S.at(d, F_DX), dy = S.at(d, F_DY), dz = S.at(d, F_DZ);
@@ -1196,10 +1252,15 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
         const int f0 = __builtin_amdgcn_readfirstlane(f);
         if (f == f0) {
           const Params q = frame_view(p0, f0);
-          double ox, oy, oz, dx, dy, dz;
-          load_ray(q, i, ox, oy, oz, dx, dy, dz);
+          // a chain deferred for depth (rays and hits counted through the same level) resumes from
+          // its record when it has one
+          const bool resume = rays_through >= 0 && rays_through == hits_through && item < p.rec_cap &&
+                              rays_through == RTX_DEEP_LEVELS;
+          double ox = 0.0, oy = 0.0, oz = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
+          if (!resume) load_ray(q, i, ox, oy, oz, dx, dy, dz);
           double cr, cg, cb;
-          trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through);
+          trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through,
+                        resume ? p.records + item * kRecWords : nullptr);
           write_out(q, i, cr, cg, cb);
           todo = false;
         }
@@ -1314,10 +1375,6 @@ inline void prof_next() {
   g_prof.on = false;
 }
 
-#ifndef RTX_DEEP_LEVELS
-#define RTX_DEEP_LEVELS 5  // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
-                           // 8-level instantiation spills, 3 defers too many pixels)
-#endif
 #ifndef RTX_CAPPED_MAX
 #define RTX_CAPPED_MAX RTX_FAST_MAX_BOUNCES  // caps rendered entirely by k_render_fast<cap>
 #endif
@@ -1359,9 +1416,18 @@ int64_t workers_for(int64_t n, int max_bounces) {
 
 size_t list_bytes(int64_t n) { return (size_t)n * sizeof(int64_t); }
 
+int64_t records_for(int64_t n, int max_bounces) {  // resume records: only when chains are deferred for depth
+  const bool capped = max_bounces >= 0 && max_bounces <= RTX_CAPPED_MAX;
+  return capped ? 0 : (n < kMaxRecords ? n : kMaxRecords);
+}
+
+size_t records_bytes(int64_t n, int max_bounces) {
+  return (((size_t)records_for(n, max_bounces) * kRecWords * sizeof(double)) + 255) / 256 * 256;
+}
+
 size_t ws_bytes(int64_t n, int max_bounces) {
   const size_t stack = (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
-  return RTX_WS_HDR_BYTES + ((list_bytes(n) + 255) / 256) * 256 + stack;
+  return RTX_WS_HDR_BYTES + ((list_bytes(n) + 255) / 256) * 256 + records_bytes(n, max_bounces) + stack;
 }
 
 template <int B>
@@ -1403,7 +1469,10 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   if (workspace_bytes < need) return fail(RTX_E_WORKSPACE, "workspace too small%s (need %lld bytes)", "", (long long)need);
   p.ws = (uint8_t*)workspace;
   p.list_cap = n_all;
-  p.stack = (double*)(p.ws + RTX_WS_HDR_BYTES + ((list_bytes(n_all) + 255) / 256) * 256);
+  uint8_t* const list_end = p.ws + RTX_WS_HDR_BYTES + ((list_bytes(n_all) + 255) / 256) * 256;
+  p.records = (double*)list_end;
+  p.rec_cap = records_for(n_all, p.max_bounces);
+  p.stack = (double*)(list_end + records_bytes(n_all, p.max_bounces));
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
   const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_CAPPED_MAX;
