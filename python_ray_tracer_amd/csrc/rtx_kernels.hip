@@ -75,6 +75,9 @@ constexpr int kDeepWorkers = RTX_DEEP_WORKERS;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
+#ifndef RTX_DEEP_WAVES
+#define RTX_DEEP_WAVES 3  // the same for the DEEP instantiation (records + continuation need registers)
+#endif
 #ifndef RTX_FAST_WAVES
 #define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
 #endif
@@ -86,7 +89,7 @@ typedef const double __attribute__((address_space(4))) cdouble;
 struct Params {
   const double* scene;
   int nsph;
-  int mode;  // 0: camera rays, 1: explicit rays
+  int mode;  // 0: camera rays, 1: explicit rays, 2: continuation of deferred chains (in_list)
   // camera mode
   int width, height, row_block, n_parts, part, n_rows;
   // explicit-ray mode
@@ -99,8 +102,19 @@ struct Params {
   void* out;
   int out_kind;
   uint8_t* ws;
-  int64_t list_cap;
-  double* records;   // resume records of deep deferrals (list slot -> record), rec_cap of them
+  int64_t list_cap;  // capacity of each deferred list
+  // Deferred lists (workspace). A launch appends to dlist (counter dcount); a chain deferred for
+  // depth after level drec_level also gets a resume record (slot < rec_cap) in drec. The
+  // continuation pass (mode 2) and the general kernel read in_list (counter in_count), whose deep
+  // entries of level in_level resume from in_rec.
+  uint64_t* dlist;
+  uint32_t* dcount;
+  double* drec;
+  int drec_level;
+  const uint64_t* in_list;
+  const uint32_t* in_count;
+  const double* in_rec;
+  int in_level;
   int64_t rec_cap;
   double* stack;
   int64_t n_workers;
@@ -112,9 +126,6 @@ struct Params {
   int64_t scene_stride;
   int n_frames;
   int frame;  // set per block / per deferred ray (kernel side)
-  // the cap exceeds the fast kernel's levels (max_bounces > RTX_FAST_MAX_BOUNCES or unbounded):
-  // k_render_fast defers a pixel whose reflection chain is still alive after its last level
-  int deep_defer;
 };
 
 // Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
@@ -131,8 +142,21 @@ constexpr int kHitsShift = 60;
                            // 8-level instantiation spills, 3 defers too many pixels)
 #endif
 constexpr int kRecLevelWords = 5;
-constexpr int kRecWords = 6 + kRecLevelWords * (RTX_DEEP_LEVELS + 1);
+__host__ __device__ constexpr int rec_words(int level) { return 6 + kRecLevelWords * (level + 1); }
+constexpr int kDeepLevel2 = 2 * RTX_DEEP_LEVELS + 1;  // deferral level of the continuation pass
+static_assert(kDeepLevel2 + 1 < 16, "deferred-entry level fields hold 4 bits");
 constexpr int64_t kMaxRecords = int64_t(1) << 18;
+
+// append one entry to the launch's deferred list; returns its slot (or -1 when the list is full)
+__device__ __forceinline__ int64_t append_deferred(const Params& p, uint64_t entry) {
+  const uint32_t slot = atomicAdd(p.dcount, 1u);
+  if ((int64_t)slot < p.list_cap) {
+    p.dlist[slot] = entry;
+    return slot;
+  }
+  atomicOr((uint32_t*)p.ws + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
+  return -1;
+}
 __device__ __forceinline__ uint64_t deferred_entry(int64_t i, int frame, int rays_through, int hits_through) {
   return (uint64_t)i | ((uint64_t)frame << kFrameShift) | ((uint64_t)(rays_through + 1) << kRaysShift) |
          ((uint64_t)(hits_through + 1) << kHitsShift);
@@ -863,19 +887,24 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 }
 
 // ------------------------------------------------------------------------------------------
-// k_render_fast<B, LDS>
+// k_render_fast<B, LDS, DEEP>
 // ------------------------------------------------------------------------------------------
 
-// One block tile: (bx, by) in camera mode, block bx of 256 rays in explicit-ray mode. `first`: the
-// block's first tile, whose level-0 nearest-hit test overlaps the LDS staging of the scene table.
-template <int B, bool LDS>
+// One block tile: (bx, by) in camera mode, block bx of 256 rays in explicit-ray mode, 256 entries
+// of in_list in continuation mode. `first`: the block's first tile, whose level-0 nearest-hit test
+// overlaps the LDS staging of the scene table. DEEP (caps above 8 or none): chains still alive
+// after B levels are deferred with a resume record, and the continuation mode exists; the capped
+// instantiations compile none of it.
+template <int B, bool LDS, bool DEEP>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
 
-  int64_t i;
+  int64_t i = 0;
   bool active;
+  int kb = 0;                  // absolute level of this launch's first ray (mode 2: the resumed level)
+  const double* rin = nullptr;  // mode 2: the chain's resume record (levels 0..kb-1)
   if (p.mode == 0) {
     // kWavesX x kWavesY waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -883,9 +912,24 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     const int lr = by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
-  } else {
+  } else if (!DEEP || p.mode == 1) {
     i = (int64_t)bx * kFastBlock + threadIdx.x;
     active = i < p.n;
+  } else {  // continuation: entry `item` of in_list
+    const int64_t item = (int64_t)bx * kFastBlock + threadIdx.x;
+    active = item < (int64_t)*p.in_count;
+    if (active) {
+      const uint64_t e = p.in_list[item];
+      i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
+      const int rt = (int)((e >> kRaysShift) & 0xF) - 1, ht = (int)((e >> kHitsShift) & 0xF) - 1;
+      if (rt == p.in_level && ht == rt && item < p.rec_cap) {
+        rin = p.in_rec + item * rec_words(p.in_level);
+        kb = rt + 1;
+      } else {  // a tie, or a chain without a record: on to the general kernel unchanged
+        append_deferred(p, e);
+        active = false;
+      }
+    }
   }
   const bool cam0 = (p.mode == 0);
 #ifdef RTX_WAVE_TIMES  // the wave-timing diagnostic borrows the stats buffer
@@ -900,11 +944,18 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   int hit = -1;
   bool tie = false;
   if (active) {
-    load_ray(p, i, ox, oy, oz, dx, dy, dz);
+    if (rin) {
+      ox = rin[0]; oy = rin[1]; oz = rin[2];
+      dx = rin[3]; dy = rin[4]; dz = rin[5];
+    } else {
+      load_ray(p, i, ox, oy, oz, dx, dy, dz);
+    }
     if (st) {
-      stat_add(st, RTX_S_PIXELS, 1);
-      stat_add(st, RTX_S_RAYS + 0, 1);
-      stat_wave(st, RTX_S_WTRACE + 0);
+      if (!rin) stat_add(st, RTX_S_PIXELS, 1);
+      if (kb < RTX_S_LEVELS) {
+        stat_add(st, RTX_S_RAYS + kb, 1);
+        stat_wave(st, RTX_S_WTRACE + kb);
+      }
     }
     if (sc[RTX_H_NNODES] != 0.0) {
       if (cam0) {
@@ -939,14 +990,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     if (tie) {  // several shapes shaded and summed: the general kernel takes this ray
       deferred = true;
-      rays_through = k;
-      hits_through = k - 1;
+      rays_through = kb + k;
+      hits_through = kb + k - 1;
       if (st) stat_add(st, RTX_S_TIES, 1);
       break;
     }
-    if (st && k < RTX_S_LEVELS) {
-      stat_add(st, RTX_S_HITS + k, 1);
-      stat_wave(st, RTX_S_WSHADE + k);
+    if (st && kb + k < RTX_S_LEVELS) {
+      stat_add(st, RTX_S_HITS + kb + k, 1);
+      stat_wave(st, RTX_S_WSHADE + kb + k);
     }
     Hit s;
     if constexpr (LDS) {
@@ -955,37 +1006,34 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
     }
     const bool weighted = s.lit && s.g != 0.0;
-    if (weighted && k >= B && p.deep_defer) {  // the chain goes on beyond this kernel's levels
-      // k == B here: levels 0..B-1 are in the shift register (slot j = level B-1-j), level B in s
+    // the cap itself (absolute level; a continuation pass may run into a cap of 9 or 10)
+    const bool at_cap = DEEP && p.max_bounces >= 0 && kb + k >= p.max_bounces;
+    if (DEEP && weighted && k >= B && !at_cap) {  // the chain goes on beyond this kernel's levels
+      // k == B: levels kb..kb+B-1 are in the shift register (slot j = level kb+B-1-j), kb+B in s
       deferred = true;
       appended = true;
-      rays_through = hits_through = B;
-      uint32_t* hdr = (uint32_t*)p.ws;
-      const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
-      if ((int64_t)slot < p.list_cap) {
-        ((uint64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = deferred_entry(i, p.frame, B, B);
-        if constexpr (B == RTX_DEEP_LEVELS) {
-          if ((int64_t)slot < p.rec_cap) {
-          double* rec = p.records + (int64_t)slot * kRecWords;
-          double rx = dx, ry = dy, rz = dz;
-          reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
-          rec[0] = s.qx; rec[1] = s.qy; rec[2] = s.qz;
-          rec[3] = rx; rec[4] = ry; rec[5] = rz;
-          double* lv = rec + 6 + kRecLevelWords * B;
-          lv[0] = s.dli; lv[1] = s.di; lv[2] = s.spec; lv[3] = s.va; lv[4] = (double)(hit | (s.chk ? 0x10000 : 0));
+      rays_through = hits_through = kb + B;
+      const int64_t slot = append_deferred(p, deferred_entry(i, p.frame, kb + B, kb + B));
+      if (p.drec && slot >= 0 && slot < p.rec_cap && kb + B == p.drec_level) {
+        double* rec = p.drec + slot * rec_words(kb + B);
+        double rx = dx, ry = dy, rz = dz;
+        reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
+        rec[0] = s.qx; rec[1] = s.qy; rec[2] = s.qz;
+        rec[3] = rx; rec[4] = ry; rec[5] = rz;
+        for (int w = 0; w < kRecLevelWords * kb; ++w) rec[6 + w] = rin[6 + w];  // levels 0..kb-1
+        double* lv = rec + 6 + kRecLevelWords * (kb + B);
+        lv[0] = s.dli; lv[1] = s.di; lv[2] = s.spec; lv[3] = s.va; lv[4] = (double)(hit | (s.chk ? 0x10000 : 0));
+        if constexpr (B > 0) {
 #pragma unroll
           for (int j = 0; j < NS; ++j) {
-            double* lj = rec + 6 + kRecLevelWords * (B - 1 - j);
+            double* lj = rec + 6 + kRecLevelWords * (kb + B - 1 - j);
             lj[0] = sDli[j]; lj[1] = sDi[j]; lj[2] = sSpec[j]; lj[3] = sVa[j]; lj[4] = (double)sKey[j];
           }
-          }
         }
-      } else {
-        atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
       }
       break;
     }
-    if (!weighted || k >= B) {
+    if (!weighted || k >= B || at_cap) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
       const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
       hit_color(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.chk, s.lit, weighted, s.spec,
@@ -1005,9 +1053,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     ox = s.qx;
     oy = s.qy;
     oz = s.qz;
-    if (st && k + 1 < RTX_S_LEVELS) {
-      stat_add(st, RTX_S_RAYS + k + 1, 1);
-      stat_wave(st, RTX_S_WTRACE + k + 1);
+    if (st && kb + k + 1 < RTX_S_LEVELS) {
+      stat_add(st, RTX_S_RAYS + kb + k + 1, 1);
+      stat_wave(st, RTX_S_WTRACE + kb + k + 1);
     }
     if (sc[RTX_H_NNODES] != 0.0) {
       nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
@@ -1019,16 +1067,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   }
 
   if (deferred) {
-    if (!appended) {  // a tie (deep deferrals were appended with their resume record)
-      uint32_t* hdr = (uint32_t*)p.ws;
-      const uint32_t slot = atomicAdd(hdr + RTX_WS_COUNT, 1u);
-      if ((int64_t)slot < p.list_cap) {
-        ((uint64_t*)(p.ws + RTX_WS_HDR_BYTES))[slot] = deferred_entry(i, p.frame, rays_through, hits_through);
-      } else {
-        atomicOr(hdr + RTX_WS_STATUS, (uint32_t)RTX_ST_LIST_OVERFLOW);
-      }
-    }
-    if (st) stat_add(st, RTX_S_DEFERRED, 1);
+    // a tie (deep deferrals were appended with their resume record)
+    if (!appended) append_deferred(p, deferred_entry(i, p.frame, rays_through, hits_through));
+    if (st && !rin) stat_add(st, RTX_S_DEFERRED, 1);
     return;
   }
   // fold back (shader.py:106-110): col_k = ((A_k + (spec_k + col_{k+1}*0.5) * g_k) + I_k); the
@@ -1044,11 +1085,19 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       sKey[j] = sKey[j + 1];
     }
   }
+  if constexpr (DEEP) {  // a continued chain: fold on through the levels of its record (same fold)
+    for (int l = kb - 1; l >= 0; --l) {
+      const double* lv = rin + 6 + kRecLevelWords * l;
+      const int key = (int)lv[4];
+      hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, lv[0], lv[1], (key >> 16) != 0, true, true, lv[2], lv[3],
+                cr, cg, cb, cr, cg, cb);
+    }
+  }
   write_out(p, i, cr, cg, cb);
 }
 
-template <int B, bool LDS>
-__global__ __launch_bounds__(kFastBlock, RTX_FAST_WAVES) void k_render_fast(Params p0) {
+template <int B, bool LDS, bool DEEP>
+__global__ __launch_bounds__(kFastBlock, DEEP ? RTX_DEEP_WAVES : RTX_FAST_WAVES) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
@@ -1060,14 +1109,23 @@ __global__ __launch_bounds__(kFastBlock, RTX_FAST_WAVES) void k_render_fast(Para
   const int64_t wslot = RTX_S_WORDS + 2 * ((((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * kFastWaves + (threadIdx.x >> 6));
   if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot] = __builtin_amdgcn_s_memrealtime();
 #endif
+  if constexpr (DEEP) {
+    if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
+      const int64_t count = (int64_t)*p.in_count;
+      for (int64_t t = blockIdx.x; t * kFastBlock < count; t += gridDim.x) {
+        fast_tile<B, LDS, DEEP>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+      }
+      return;
+    }
+  }
   if (p.n_tiles_x == 0) {  // one tile per block
     // Bottom tile rows are dispatched first: they hold the ground and the spheres, whose pixels
     // run long bounce chains, while sky rows finish at level 0 and so fill the end of the grid
     // (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on the order.
 #ifdef RTX_FORWARD_ROWS
-    fast_tile<B, LDS>(p, blockIdx.x, blockIdx.y, true, lds_tab);
+    fast_tile<B, LDS, DEEP>(p, blockIdx.x, blockIdx.y, true, lds_tab);
 #else
-    fast_tile<B, LDS>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
+    fast_tile<B, LDS, DEEP>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 #endif
 #ifdef RTX_WAVE_TIMES
     if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1079,7 +1137,7 @@ __global__ __launch_bounds__(kFastBlock, RTX_FAST_WAVES) void k_render_fast(Para
   const int nt = p.n_tiles_x * p.n_tiles_y;
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
     const int row = t / p.n_tiles_x;
-    fast_tile<B, LDS>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, t == (int)blockIdx.x, lds_tab);
+    fast_tile<B, LDS, DEEP>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, t == (int)blockIdx.x, lds_tab);
   }
 }
 
@@ -1234,13 +1292,13 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const Params& p = p0;
   uint32_t* hdr = (uint32_t*)p.ws;
-  int64_t count = (int64_t)hdr[RTX_WS_COUNT];
+  int64_t count = (int64_t)*p.in_count;
   if (count > p.list_cap) count = p.list_cap;
-  const int64_t* list = (const int64_t*)(p.ws + RTX_WS_HDR_BYTES);
+  const uint64_t* list = p.in_list;
   if (w < p.n_workers) {
     Stack S{p.stack, p.n_workers, w};
     for (int64_t item = w; item < count; item += p.n_workers) {
-      const uint64_t e = (uint64_t)list[item];
+      const uint64_t e = list[item];
       const int64_t i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
       const int f = (int)((e >> kFrameShift) & 0xFFFF);
       const int rays_through = (int)((e >> kRaysShift) & 0xF) - 1;
@@ -1254,13 +1312,13 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
           const Params q = frame_view(p0, f0);
           // a chain deferred for depth (rays and hits counted through the same level) resumes from
           // its record when it has one
-          const bool resume = rays_through >= 0 && rays_through == hits_through && item < p.rec_cap &&
-                              rays_through == RTX_DEEP_LEVELS;
+          const bool resume = p.in_rec && rays_through == p.in_level && hits_through == rays_through &&
+                              item < p.rec_cap;
           double ox = 0.0, oy = 0.0, oz = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
           if (!resume) load_ray(q, i, ox, oy, oz, dx, dy, dz);
           double cr, cg, cb;
           trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through,
-                        resume ? p.records + item * kRecWords : nullptr);
+                        resume ? p.in_rec + item * rec_words(p.in_level) : nullptr);
           write_out(q, i, cr, cg, cb);
           todo = false;
         }
@@ -1271,10 +1329,12 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
   // (every block has read it before arriving; the next kernel on the stream sees the store)
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (gridDim.x == 1) {  // one block: no other reader of the counter
+    if (gridDim.x == 1) {  // one block: no other reader of the counters
       hdr[RTX_WS_COUNT] = 0u;
+      hdr[RTX_WS_COUNT2] = 0u;
     } else if (atomicAdd(hdr + RTX_WS_DONE, 1u) == gridDim.x - 1) {
       hdr[RTX_WS_COUNT] = 0u;
+      hdr[RTX_WS_COUNT2] = 0u;
       hdr[RTX_WS_DONE] = 0u;
     }
   }
@@ -1421,24 +1481,39 @@ int64_t records_for(int64_t n, int max_bounces) {  // resume records: only when 
   return capped ? 0 : (n < kMaxRecords ? n : kMaxRecords);
 }
 
-size_t records_bytes(int64_t n, int max_bounces) {
-  return (((size_t)records_for(n, max_bounces) * kRecWords * sizeof(double)) + 255) / 256 * 256;
+size_t round256(size_t b) { return (b + 255) / 256 * 256; }
+
+// Workspace: header | list 1 | (deep chains:) list 2 | records of level RTX_DEEP_LEVELS | records of
+// level kDeepLevel2 | general-kernel stacks
+struct WsLayout {
+  size_t list1, list2, rec1, rec2, stack, total;
+};
+WsLayout ws_layout(int64_t n, int max_bounces) {
+  WsLayout w{};
+  const int64_t nrec = records_for(n, max_bounces);
+  w.list1 = RTX_WS_HDR_BYTES;
+  w.list2 = w.list1 + round256(list_bytes(n));
+  w.rec1 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
+  w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(RTX_DEEP_LEVELS) * sizeof(double));
+  w.stack = w.rec2 + round256((size_t)nrec * rec_words(kDeepLevel2) * sizeof(double));
+  w.total = w.stack + (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
+  return w;
 }
 
-size_t ws_bytes(int64_t n, int max_bounces) {
-  const size_t stack = (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
-  return RTX_WS_HDR_BYTES + ((list_bytes(n) + 255) / 256) * 256 + records_bytes(n, max_bounces) + stack;
-}
+size_t ws_bytes(int64_t n, int max_bounces) { return ws_layout(n, max_bounces).total; }
 
-template <int B>
+template <int B, bool DEEP = false>
 void launch_fast_b(const Params& p, dim3 grid, hipStream_t s) {
   if (p.nsph <= kLdsMaxSpheres) {
     const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double);
-    hipLaunchKernelGGL((k_render_fast<B, true>), grid, dim3(kFastBlock), lds, s, p);
+    hipLaunchKernelGGL((k_render_fast<B, true, DEEP>), grid, dim3(kFastBlock), lds, s, p);
   } else {
-    hipLaunchKernelGGL((k_render_fast<B, false>), grid, dim3(kFastBlock), 0, s, p);
+    hipLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0, s, p);
   }
 }
+
+// caps above RTX_CAPPED_MAX or none: RTX_DEEP_LEVELS levels, longer chains deferred with a record
+void launch_fast_deep(const Params& p, dim3 grid, hipStream_t s) { launch_fast_b<RTX_DEEP_LEVELS, true>(p, grid, s); }
 
 void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
   switch (B) {
@@ -1469,14 +1544,17 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   if (workspace_bytes < need) return fail(RTX_E_WORKSPACE, "workspace too small%s (need %lld bytes)", "", (long long)need);
   p.ws = (uint8_t*)workspace;
   p.list_cap = n_all;
-  uint8_t* const list_end = p.ws + RTX_WS_HDR_BYTES + ((list_bytes(n_all) + 255) / 256) * 256;
-  p.records = (double*)list_end;
+  const WsLayout lay = ws_layout(n_all, p.max_bounces);
+  uint32_t* const hdr = (uint32_t*)p.ws;
+  uint64_t* const list1 = (uint64_t*)(p.ws + lay.list1);
+  uint64_t* const list2 = (uint64_t*)(p.ws + lay.list2);
+  double* const rec1 = (double*)(p.ws + lay.rec1);
+  double* const rec2 = (double*)(p.ws + lay.rec2);
   p.rec_cap = records_for(n_all, p.max_bounces);
-  p.stack = (double*)(list_end + records_bytes(n_all, p.max_bounces));
+  p.stack = (double*)(p.ws + lay.stack);
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
   const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_CAPPED_MAX;
-  p.deep_defer = capped ? 0 : 1;
   p.n_workers = workers_for(n_all, p.max_bounces);
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
@@ -1492,11 +1570,42 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
       p.n_tiles_x = p.n_tiles_y = 0;
       grid = dim3((unsigned)tx, (unsigned)ty, (unsigned)p.n_frames);
     }
+    p.dlist = list1;
+    p.dcount = hdr + RTX_WS_COUNT;
+    p.drec = capped ? nullptr : rec1;
+    p.drec_level = RTX_DEEP_LEVELS;
     prof_mark(0, s);
-    launch_fast(capped ? p.max_bounces : RTX_DEEP_LEVELS, p, grid, s);
+    if (capped) {
+      launch_fast(p.max_bounces, p, grid, s);
+    } else {
+      launch_fast_deep(p, grid, s);
+    }
     prof_mark(1, s);
     prof_next();
     if (int e = check_launch("k_render_fast")) return e;
+  }
+  p.in_list = list1;
+  p.in_count = hdr + RTX_WS_COUNT;
+  p.in_rec = capped ? nullptr : rec1;
+  p.in_level = RTX_DEEP_LEVELS;
+  if (!capped && p.n_frames == 1) {
+    // continuation pass: chains deferred for depth go on for RTX_DEEP_LEVELS + 1 more levels in the
+    // register-resident kernel; ties and what is still alive after it go to the general kernel
+    Params q = p;
+    q.mode = 2;
+    q.n_tiles_x = q.n_tiles_y = 0;
+    q.dlist = list2;
+    q.dcount = hdr + RTX_WS_COUNT2;
+    q.drec = rec2;
+    q.drec_level = kDeepLevel2;
+    const int64_t tiles = (n_all + kFastBlock - 1) / kFastBlock;
+    const int64_t cap = 4 * (int64_t)device_cus();
+    launch_fast_deep(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
+    if (int e = check_launch("k_render_fast (continuation)")) return e;
+    p.in_list = list2;
+    p.in_count = hdr + RTX_WS_COUNT2;
+    p.in_rec = rec2;
+    p.in_level = kDeepLevel2;
   }
   // deferred rays: ties, and chains longer than the fast kernel's levels
   hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);
