@@ -86,6 +86,12 @@ def test_ties_take_the_general_kernel(hip, golden_meta, golden_renders):
     assert np.abs(got - golden_renders["ties_64x36_B2"]).max() <= ATOL
     s = r.stats()
     assert s["deferred"] > 100 and s["ties"] >= s["deferred"]
+    # no cap: ties deferred by the first pass are forwarded through the continuation pass
+    r, got = _render(hip, case["spec"], None, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(case["spec"]), None, stats=st)
+    assert np.abs(got - want).max() <= ATOL
+    assert r.stats()["rays"] == st.rays and r.stats()["hits"] == st.hits
 
 
 @pytest.mark.parametrize("B", [0, 1, 2, 4, 5, 6, 7, 8, 9, 12])
@@ -195,6 +201,11 @@ def test_explicit_rays_and_intersect(hip, golden_meta):
     o = [np.full(d[0].shape, v) + rng.uniform(-0.1, 0.1, d[0].shape) for v in sc.cam]
     got = r.raytrace_scene(hip.HipVector3D(*o), hip.HipVector3D(*d), scene).data.cpu().numpy()
     want = np.stack(O.trace(sc, tuple(o), d, 3))
+    assert np.abs(got - want).max() <= ATOL
+    # the same rays with no bounce cap (the reference default): explicit rays through the deep
+    # deferral, the continuation pass and the general kernel
+    got = hip.HipRenderer().raytrace_scene(hip.HipVector3D(*o), hip.HipVector3D(*d), scene).data.cpu().numpy()
+    want = np.stack(O.trace(sc, tuple(o), d, None))
     assert np.abs(got - want).max() <= ATOL
     # intersect known answers
     for k in json.loads((GOLDEN / "intersect_kat.json").read_text()):
@@ -315,3 +326,17 @@ def test_vector_algebra_on_device(hip):
     got = [c.cpu().numpy() for c in v.norm().components()]
     assert all(np.array_equal(g, w) for g, w in zip(got, want))
     assert np.array_equal(abs(v).cpu().numpy(), (a[0] * a[0] + a[1] * a[1]) + a[2] * a[2])
+
+
+@pytest.mark.parametrize("B", [3, None])
+def test_large_scene_without_lds_table(hip, B):
+    """More than 128 spheres: the fast kernel reads materials from HBM instead of its LDS copy (the
+    other instantiation), the culling tree has many levels; capped and unbounded (continuation and
+    general kernel) against the oracle."""
+    spec = scenes.random_spec(150, 4, 72, 40)
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL
+    assert np.array_equal(O.to_uint8(got, 72, 40), O.to_uint8(want, 72, 40))
+    assert r.stats()["rays"] == st.rays
