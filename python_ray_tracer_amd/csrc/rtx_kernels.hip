@@ -34,6 +34,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/rtx_hip.h"
@@ -60,6 +61,18 @@ constexpr int kWavesY = kFastWaves / kWavesX;
 constexpr int kTileW = kWavesX * kWaveW;
 constexpr int kTileH = kWavesY * kWaveH;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
+// k_render_fast single-frame launches of scenes with at least this many spheres: persistent waves
+// fetching wave tiles (A/B: 65 spheres -14%, 17 spheres +-0, 3-16 spheres without the culling tree
+// +12%: their tiles are short, so the ramp-up of the fetch counters and the drain cost more than
+// the balancing gains)
+#ifndef RTX_PERSIST_MIN_SPHERES
+#define RTX_PERSIST_MIN_SPHERES 32
+#endif
+#ifndef RTX_FETCH_COUNTERS
+#define RTX_FETCH_COUNTERS 32  // tile counters (one 128-byte line each) shared round-robin by the waves
+#endif
+constexpr int kMaxFetch = RTX_FETCH_COUNTERS;
+constexpr int kFetchStride = 32;  // uint32 words between counters
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
 // general-kernel threads: ties only (caps <= RTX_FAST_MAX_BOUNCES; an empty launch costs more with
@@ -121,6 +134,9 @@ struct Params {
   int stack_levels;
   unsigned long long* stats;
   int n_tiles_x, n_tiles_y;  // persistent launch of k_render_fast (0: one tile per block)
+  // persistent waves (n_fetch > 0): wave tiles (kWaveW x kWaveH) handed out by n_fetch counters
+  uint32_t* fetch;
+  int n_fetch;
   // multi-frame launch (rtx_render_frames): frame f reads scene + f * scene_stride and writes
   // out + f * (one frame's output); n counts the pixels of ONE frame
   int64_t scene_stride;
@@ -245,6 +261,30 @@ __device__ __forceinline__ void norm3(double& x, double& y, double& z) {
   z = z * r;
 }
 
+// 1.0 / where(mag == 0, 1, mag), mag = sqrt(d), for d = |v|^2 within 2^-30 of 1: the norm of a
+// vector that is already unit up to rounding (a direction normalised before, or the reflection of
+// one). Write d = 1 + j 2^-53 (j an integer, even when positive). The correctly rounded sqrt(d) is
+// 1 + floor(j/4) 2^-52 for j >= 0 and 1 - ceil(-j/2) 2^-53 for j < 0, and the correctly rounded
+// reciprocal of either is 1 - floor(j/4) 2^-52: the second-order terms stay far below half an ulp
+// for |j| <= 2^23. (d - 1) * 2^51 = j/4 exactly, floor is exact and so is the fma, so the result is
+// bit-identical to div(1, sqrt(d)) (tests/test_unit_norm.py checks every such d against IEEE sqrt
+// and division; k_selftest_math checks this path on the device).
+__device__ __forceinline__ double inv_mag_near1(double d) {
+  return __builtin_fma(-__builtin_floor((d - 1.0) * 0x1.0p51), 0x1.0p-52, 1.0);
+}
+__device__ __forceinline__ double inv_mag_unit(double d) {
+  // wave-uniform: the closed form unless some active lane is out of its range
+  if (__ballot(!(fabs(d - 1.0) <= 0x1.0p-30)) == 0) return inv_mag_near1(d);
+  return inv_mag(d);
+}
+__device__ __forceinline__ void norm3_unit(double& x, double& y, double& z) {
+  // NumpyVector3D.norm (base.py:61-64) of a vector expected to be unit up to rounding
+  const double r = inv_mag_unit(dot3(x, y, z, x, y, z));
+  x = x * r;
+  y = y * r;
+  z = z * r;
+}
+
 // np.clip(x, 0, 1) and np.maximum(x, 0) as v_max_f64 / v_min_f64. They differ from the reference
 // only for NaN inputs and in the sign of a zero result, which never reaches the output: every such
 // value is squared, scaled into a sum with the 0.004 ambient term, or compared with <= 0.
@@ -260,6 +300,18 @@ __device__ __forceinline__ int trunc_parity(double x) {
   return (x == x) && (h != trunc(h));
 }
 
+// b >= 0 and c >= 0 (the sphere lies behind an origin outside it): the reference's root is never
+// positive, so the test is FARAWAY without a square root. Proof: disc = fl(fl(b*b) - 4c) <= fl(b*b),
+// and for b >= 0 with b*b finite (b <= 1e150) the correctly rounded sqrt(fl(b*b)) is b itself
+// (b*b*(1 + 2^-53) has a root below b + ulp(b)/2), so sq <= b and s1 = (-b + sq) / 2 <= 0.
+__device__ __forceinline__ bool behind(double b, double c) {
+#ifdef RTX_NO_BEHIND
+  return false;
+#else
+  return b >= 0.0 && c >= 0.0 && b <= 1e150;
+#endif
+}
+
 // NumpySphere.intersect, shape.py:28-51, for a ray with precomputed oo = O.O.
 // b = 2 * D.(O - C);  c = ((C.C + O.O) - 2 * C.O) - r*r;  disc = b^2 - 4c.
 template <typename P>
@@ -270,7 +322,7 @@ __device__ __forceinline__ double isect(const P* g, double ox, double oy, double
   const double c = ((g[RTX_G_CC] + oo) - 2.0 * dot3(cx, cy, cz, ox, oy, oz)) - g[RTX_G_RR];
   const double disc = (b * b) - (4.0 * c);
   double t = FARAWAY;
-  if (disc > 0.0) {  // np.where((disc > 0) & (sol > 0), sol, FARAWAY); sqrt(max(0, disc)) == sqrt(disc) here
+  if (disc > 0.0 && !behind(b, c)) {  // np.where((disc > 0) & (sol > 0), sol, FARAWAY); sqrt(max(0, disc)) == sqrt(disc) here
     const double sq = sqrt_cr(disc);
     const double s0 = (-b - sq) * 0.5;  // == / 2 exactly
     const double s1 = (-b + sq) * 0.5;
@@ -285,18 +337,21 @@ __device__ __forceinline__ double isect(const P* g, double ox, double oy, double
 // scalar loads share one wait): isect_disc computes b and the discriminant, isect_sol the rest.
 template <typename P>
 __device__ __forceinline__ void isect_disc(const P* g, double ox, double oy, double oz, double oo, double dx,
-                                           double dy, double dz, double& b, double& disc) {
+                                           double dy, double dz, double& b, double& disc, bool& skip) {
   const double cx = g[RTX_G_CX], cy = g[RTX_G_CY], cz = g[RTX_G_CZ];
   b = 2.0 * dot3(dx, dy, dz, ox - cx, oy - cy, oz - cz);
   const double c = ((g[RTX_G_CC] + oo) - 2.0 * dot3(cx, cy, cz, ox, oy, oz)) - g[RTX_G_RR];
   disc = (b * b) - (4.0 * c);
+  skip = !(disc > 0.0) || behind(b, c);
 }
 // level-0 camera origin: O - C from uniform values, c precomputed on the host (same expressions)
 template <typename P>
 __device__ __forceinline__ void isect_disc_cam(const P* g, double ox, double oy, double oz, double dx, double dy,
-                                               double dz, double& b, double& disc) {
+                                               double dz, double& b, double& disc, bool& skip) {
   b = 2.0 * dot3(dx, dy, dz, ox - g[RTX_G_CX], oy - g[RTX_G_CY], oz - g[RTX_G_CZ]);
-  disc = (b * b) - (4.0 * g[RTX_G_C0]);
+  const double c = g[RTX_G_C0];
+  disc = (b * b) - (4.0 * c);
+  skip = !(disc > 0.0) || behind(b, c);
 }
 // The rest of the test, as a root and a validity flag instead of the FARAWAY sentinel (no f64
 // selects of a non-inline constant): valid <=> the reference returns the root, not FARAWAY. With
@@ -309,19 +364,19 @@ __device__ __forceinline__ double isect_sol(double b, double disc, bool& valid) 
   valid = disc > 0.0 && s1 > 0.0;
   return s0 > 0.0 ? s0 : s1;
 }
-// one sphere; the square root runs only if the discriminant is positive in some lane
-__device__ __forceinline__ double isect_one_sol(double b, double disc, bool& valid) {
+// one sphere; the square root runs only if some lane may hit (skip: disc <= 0 or behind)
+__device__ __forceinline__ double isect_one_sol(double b, double disc, bool skip, bool& valid) {
   valid = false;
   double t = 0.0;
-  if (disc > 0.0) t = isect_sol(b, disc, valid);
+  if (!skip) t = isect_sol(b, disc, valid);
   return t;
 }
-// two spheres at once; the square roots run only if either discriminant is positive (per lane)
-__device__ __forceinline__ void isect_pair_sol(double b0, double disc0, double b1, double disc1, double& t0,
-                                               bool& v0, double& t1, bool& v1) {
+// two spheres at once; the square roots run only if either test may hit (per lane)
+__device__ __forceinline__ void isect_pair_sol(double b0, double disc0, bool skip0, double b1, double disc1,
+                                               bool skip1, double& t0, bool& v0, double& t1, bool& v1) {
   v0 = v1 = false;
   t0 = t1 = 0.0;
-  if (disc0 > 0.0 || disc1 > 0.0) {
+  if (!skip0 || !skip1) {
     t0 = isect_sol(b0, disc0, v0);
     t1 = isect_sol(b1, disc1, v1);
   }
@@ -396,28 +451,30 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
     const cdouble* g1 = g0 + RTX_GEOM_WORDS;
     double b0, d0, b1, d1, t0, t1;
+    bool k0, k1;
     if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
-      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1);
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
+      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1, k1);
     } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
-      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1);
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
+      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1, k1);
     }
     bool v0, v1;
-    isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+    isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
     nearest_update(v0, t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
     nearest_update(v1, t1, (int)g1[RTX_G_IDX], tmin, hit, tie);
   }
   if (k < end) {
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
     double b0, d0;
+    bool k0;
     if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
     } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
     }
     bool v0;
-    const double t0 = isect_one_sol(b0, d0, v0);
+    const double t0 = isect_one_sol(b0, d0, k0, v0);
     nearest_update(v0, t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
   }
 }
@@ -476,9 +533,10 @@ __device__ __forceinline__ void nearest_count_bvh(const cdouble* sc, double ox, 
     for (; k < end; ++k) {
       const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
       double b0, d0;
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+      bool k0;
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
       bool v0;
-      const double t0 = isect_one_sol(b0, d0, v0);
+      const double t0 = isect_one_sol(b0, d0, k0, v0);
       count_update(v0, t0, (int)g0[RTX_G_IDX], tmin, nh, first);
     }
   };
@@ -512,9 +570,10 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
     if ((int)g0[RTX_G_IDX] == hs) continue;
     double b0, d0;
-    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+    bool k0;
+    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
     bool v0;
-    const double t0 = isect_one_sol(b0, d0, v0);
+    const double t0 = isect_one_sol(b0, d0, k0, v0);
     if (v0 && t0 < tself) lit = false;
   }
   const RaySlab rs = ray_slab(lx, ly, lz, qq);
@@ -530,18 +589,20 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
           const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
           const cdouble* g1 = g0 + RTX_GEOM_WORDS;
           double b0, d0, b1, d1, t0, t1;
-          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
-          isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
+          bool k0, k1;
+          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
+          isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1, k1);
           bool v0, v1;
-          isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+          isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
           if ((v0 && t0 < tself) || (v1 && t1 < tself)) lit = false;
         }
         if (k < end) {
           const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
           double b0, d0;
-          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+          bool k0;
+          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
           bool v0;
-          const double t0 = isect_one_sol(b0, d0, v0);
+          const double t0 = isect_one_sol(b0, d0, k0, v0);
           if (v0 && t0 < tself) lit = false;
         }
       }
@@ -568,29 +629,31 @@ __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, d
     const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
     const P* g1 = g0 + RTX_GEOM_WORDS;
     double b0, d0, b1, d1;
+    bool k0, k1;
     if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
-      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1);
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
+      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1, k1);
     } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
-      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1);
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
+      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1, k1);
     }
     double t0, t1;
     bool v0, v1;
-    isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+    isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
     nearest_update(v0, t0, s, tmin, hit, tie);
     nearest_update(v1, t1, s + 1, tmin, hit, tie);
   }
   if (s < nsph) {
     const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
     double b0, d0;
+    bool k0;
     if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0);
+      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
     } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0);
+      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
     }
     bool v0;
-    const double t0 = isect_one_sol(b0, d0, v0);
+    const double t0 = isect_one_sol(b0, d0, k0, v0);
     nearest_update(v0, t0, s, tmin, hit, tie);
   }
 }
@@ -743,10 +806,11 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
     const G* g0 = geo + j0 * RTX_GEOM_WORDS;
     const G* g1 = geo + j1 * RTX_GEOM_WORDS;
     double b0, d0, b1, d1, t0, t1;
-    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
-    isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1);
+    bool k0, k1;
+    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
+    isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1, k1);
     bool v0, v1;
-    isect_pair_sol(b0, d0, b1, d1, t0, v0, t1, v1);
+    isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
     if (shadows(v0, t0, tself, far_self) || shadows(v1, t1, tself, far_self)) {
       lit = false;
       break;
@@ -755,9 +819,10 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   if (lit && j < nshadow) {
     const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
     double b0, d0;
-    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0);
+    bool k0;
+    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
     bool v0;
-    const double t0 = isect_one_sol(b0, d0, v0);
+    const double t0 = isect_one_sol(b0, d0, k0, v0);
     if (shadows(v0, t0, tself, far_self)) lit = false;
   }
 
@@ -896,7 +961,8 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // after B levels are deferred with a resume record, and the continuation mode exists; the capped
 // instantiations compile none of it.
 template <int B, bool LDS, bool DEEP>
-__device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab) {
+__device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
+                                          bool wave_tile = false) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
@@ -907,9 +973,10 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const double* rin = nullptr;  // mode 2: the chain's resume record (levels 0..kb-1)
   if (p.mode == 0) {
     // kWavesX x kWavesY waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
+    // (wave_tile: (bx, by) is this wave's own kWaveW x kWaveH tile)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = bx * kTileW + (w % kWavesX) * kWaveW + (lane % kWaveW);
-    const int lr = by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
+    const int col = wave_tile ? bx * kWaveW + (lane % kWaveW) : bx * kTileW + (w % kWavesX) * kWaveW + (lane % kWaveW);
+    const int lr = wave_tile ? by * kWaveH + (lane / kWaveW) : by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else if (!DEEP || p.mode == 1) {
@@ -1107,7 +1174,7 @@ __global__ __launch_bounds__(kFastBlock, DEEP ? RTX_DEEP_WAVES : RTX_FAST_WAVES)
   }
 #ifdef RTX_WAVE_TIMES  // diagnostic (tools/wave_times.py): per-wave start/end, 100 MHz clock
   const int64_t wslot = RTX_S_WORDS + 2 * ((((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * kFastWaves + (threadIdx.x >> 6));
-  if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot] = __builtin_amdgcn_s_memrealtime();
+  if (p.stats && p.n_fetch == 0 && (threadIdx.x & 63) == 0) p.stats[wslot] = __builtin_amdgcn_s_memrealtime();
 #endif
   if constexpr (DEEP) {
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
@@ -1117,6 +1184,51 @@ __global__ __launch_bounds__(kFastBlock, DEEP ? RTX_DEEP_WAVES : RTX_FAST_WAVES)
       }
       return;
     }
+  }
+  if (p.n_fetch > 0) {
+    // Persistent waves fetching kWaveW x kWaveH tiles, bottom-up (longest work first, as below).
+    // Counter c (of n_fetch) hands out tiles c, c + n_fetch, ... . Waves are numbered XCD-major
+    // (pw; block b runs on XCD b % 8) and wave pw uses counter pw % n_fetch, so every counter's
+    // waves are spread over all XCDs. Wave pw renders tile pw first (static, no fetch); the next
+    // tile's atomic is always issued before the current tile renders, hiding its latency. Each
+    // wave makes exactly one out-of-range fetch, so the wave receiving a counter's last value is
+    // its last user and resets it to 0 for the next launch (no per-launch memset).
+    if constexpr (LDS) __syncthreads();  // the table staged above
+    const int lane = threadIdx.x & 63;
+    const int nc = p.n_fetch;
+    const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+    const int pw = ((int)(blockIdx.x % nx) * (int)(gridDim.x / nx) + (int)(blockIdx.x / nx)) * kFastWaves +
+                   (threadIdx.x >> 6);
+    const int waves_c = (int)(gridDim.x * kFastWaves) / nc;  // the host makes nc divide the waves per XCD
+    const int c = pw % nc;
+    const int nt = p.n_tiles_x * p.n_tiles_y;
+    const int tiles_c = (nt - c + nc - 1) / nc;
+    uint32_t* const ctr = p.fetch + c * kFetchStride;
+    uint32_t nxt = 0;
+    if (lane == 0) nxt = atomicAdd(ctr, 1u);
+    int k = pw / nc;
+    int v = 0;
+    while (k < tiles_c) {
+      const int t = c + k * nc;
+      const int row = t / p.n_tiles_x;
+#ifdef RTX_WAVE_TIMES  // per-tile start/end, slot = tile in dispatch order
+      const uint64_t ts = __builtin_amdgcn_s_memrealtime();
+#endif
+      fast_tile<B, LDS, DEEP>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
+#ifdef RTX_WAVE_TIMES
+      if (p.stats && lane == 0) {
+        p.stats[RTX_S_WORDS + 2 * t] = ts;
+        p.stats[RTX_S_WORDS + 2 * t + 1] = __builtin_amdgcn_s_memrealtime();
+      }
+#endif
+      v = __builtin_amdgcn_readfirstlane(nxt);
+      k = waves_c + v;
+      if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
+    }
+    if (k == pw / nc) v = __builtin_amdgcn_readfirstlane(nxt);  // no tile rendered: the first fetch
+    const int dyn = tiles_c > waves_c ? tiles_c - waves_c : 0;  // in-range fetches on this counter
+    if (lane == 0 && v == dyn + waves_c - 1) atomicExch(ctr, 0u);
+    return;
   }
   if (p.n_tiles_x == 0) {  // one tile per block
     // Bottom tile rows are dispatched first: they hold the ground and the spheres, whose pixels
@@ -1483,15 +1595,16 @@ int64_t records_for(int64_t n, int max_bounces) {  // resume records: only when 
 
 size_t round256(size_t b) { return (b + 255) / 256 * 256; }
 
-// Workspace: header | list 1 | (deep chains:) list 2 | records of level RTX_DEEP_LEVELS | records of
+// Workspace: header | tile counters | list 1 | (deep chains:) list 2 | records of level RTX_DEEP_LEVELS | records of
 // level kDeepLevel2 | general-kernel stacks
 struct WsLayout {
-  size_t list1, list2, rec1, rec2, stack, total;
+  size_t fetch, list1, list2, rec1, rec2, stack, total;
 };
 WsLayout ws_layout(int64_t n, int max_bounces) {
   WsLayout w{};
   const int64_t nrec = records_for(n, max_bounces);
-  w.list1 = RTX_WS_HDR_BYTES;
+  w.fetch = RTX_WS_HDR_BYTES;
+  w.list1 = w.fetch + (size_t)kMaxFetch * kFetchStride * sizeof(uint32_t);
   w.list2 = w.list1 + round256(list_bytes(n));
   w.rec1 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
   w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(RTX_DEEP_LEVELS) * sizeof(double));
@@ -1502,12 +1615,38 @@ WsLayout ws_layout(int64_t n, int max_bounces) {
 
 size_t ws_bytes(int64_t n, int max_bounces) { return ws_layout(n, max_bounces).total; }
 
+// Persistent launch (p.n_fetch > 0 on entry): as many blocks as the device holds at once, at most one
+// wave per tile; sets n_fetch to the counters in use (every counter needs at least one wave).
+template <typename K>
+dim3 persistent_grid(K kernel, size_t lds, Params& p) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kFastBlock, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const int64_t nt = (int64_t)p.n_tiles_x * p.n_tiles_y;
+  int64_t blocks = (int64_t)per_cu * device_cus();
+  const int64_t need = (nt + kFastWaves - 1) / kFastWaves;
+  if (blocks > need) blocks = need;
+  if (blocks >= 8) blocks -= blocks % 8;  // whole XCD groups (the kernel numbers waves XCD-major)
+  const int64_t per_xcd = blocks * kFastWaves / (blocks % 8 == 0 ? 8 : 1);
+  int nc = kMaxFetch;  // a power of two dividing the waves per XCD
+  while (nc > 1 && per_xcd % nc != 0) nc /= 2;
+  p.n_fetch = nc;
+  if (getenv("RTX_DEBUG_GRID"))
+    fprintf(stderr, "persistent grid: %d blocks/CU x %d CUs -> %lld blocks, %d counters, %lld tiles\n", per_cu,
+            device_cus(), (long long)blocks, p.n_fetch, (long long)nt);
+  static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "RTX_FETCH_COUNTERS must be a power of two");
+  return dim3((unsigned)blocks);
+}
+
 template <int B, bool DEEP = false>
-void launch_fast_b(const Params& p, dim3 grid, hipStream_t s) {
+void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
+  Params p = p0;
   if (p.nsph <= kLdsMaxSpheres) {
     const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double);
+    if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP>, lds, p);
     hipLaunchKernelGGL((k_render_fast<B, true, DEEP>), grid, dim3(kFastBlock), lds, s, p);
   } else {
+    if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP>, 0, p);
     hipLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0, s, p);
   }
 }
@@ -1562,7 +1701,14 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kFastBlock - 1) / kFastBlock);
     const int ty = p.mode == 0 ? (p.n_rows + kTileH - 1) / kTileH : 1;
     const int64_t nt = (int64_t)tx * ty;
-    if (RTX_TILES_PER_BLOCK > 1 && nt > RTX_TILES_PER_BLOCK) {
+    p.n_fetch = 0;
+    if (p.nsph >= RTX_PERSIST_MIN_SPHERES && p.mode == 0 && p.n_frames == 1) {
+      p.n_tiles_x = (p.width + kWaveW - 1) / kWaveW;  // wave tiles
+      p.n_tiles_y = (p.n_rows + kWaveH - 1) / kWaveH;
+      p.fetch = (uint32_t*)(p.ws + lay.fetch);
+      p.n_fetch = kMaxFetch;  // launch_fast_b sizes the grid and the counters in use
+      grid = dim3(1);
+    } else if (RTX_TILES_PER_BLOCK > 1 && nt > RTX_TILES_PER_BLOCK) {
       p.n_tiles_x = tx;
       p.n_tiles_y = ty;
       grid = dim3((unsigned)((nt + RTX_TILES_PER_BLOCK - 1) / RTX_TILES_PER_BLOCK), 1, (unsigned)p.n_frames);
@@ -1594,6 +1740,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     Params q = p;
     q.mode = 2;
     q.n_tiles_x = q.n_tiles_y = 0;
+    q.n_fetch = 0;
     q.dlist = list2;
     q.dcount = hdr + RTX_WS_COUNT2;
     q.drec = rec2;
