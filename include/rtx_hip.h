@@ -230,9 +230,11 @@ int rtx_sphere_intersect(const double* sphere, const double* origins, int64_t or
 int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, void* stream);
 
 /* Test hook: out[0:n] = the library's fast-path sqrt(a), out[n:2n] = the compiler's full sqrt(a),
- * out[2n:3n] = fast-path a/b, out[3n:4n] = full a/b. The render kernels use the fast paths
- * (correctly rounded sequences without operand scaling where it is the identity); tests require
- * each pair to agree bit for bit. */
+ * out[2n:3n] = fast-path a/b, out[3n:4n] = full a/b, out[4n:5n] = the renormalisation factor of an
+ * already-unit vector with |v|^2 = a (closed form when every lane of the wave has a within 2^-30
+ * of 1), out[5n:6n] = 1/sqrt(a) by the full expansions (a == 0: 1). out holds 6n doubles. The
+ * render kernels use the fast paths (correctly rounded sequences without operand scaling where it
+ * is the identity); tests require each pair to agree bit for bit. */
 int rtx_selftest_math(const double* a, const double* b, int64_t n, double* out, void* stream);
 
 /* Live timing of the dominant render kernel (used by bench.py for the roofline): after

@@ -685,9 +685,9 @@ template <typename M>
 __device__ __forceinline__ double specular(const M* mh, double g, double nx, double ny, double nz, double lx,
                                            double ly, double lz, double vx, double vy, double vz) {
   double Lx = lx, Ly = ly, Lz = lz;
-  norm3(Lx, Ly, Lz);  // :278 (normalised a second time)
+  norm3_unit(Lx, Ly, Lz);  // :278 (normalised a second time)
   double Vx = vx, Vy = vy, Vz = vz;
-  norm3(Vx, Vy, Vz);  // :279
+  norm3_unit(Vx, Vy, Vz);  // :279 (likewise)
   double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
   norm3(Hx, Hy, Hz);  // :280
   const double NdotV = clip01(dot3(nx, ny, nz, Vx, Vy, Vz));  // :283
@@ -863,7 +863,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
 __device__ __forceinline__ void reflect_dir(double& dx, double& dy, double& dz, double nx, double ny, double nz) {
   const double dn = dot3(dx, dy, dz, nx, ny, nz);
   double rx = dx - (nx * 2.0) * dn, ry = dy - (ny * 2.0) * dn, rz = dz - (nz * 2.0) * dn;
-  norm3(rx, ry, rz);
+  norm3_unit(rx, ry, rz);  // |D| = |N| = 1 up to rounding, so |R| too
   dx = rx;
   dy = ry;
   dz = rz;
@@ -1488,6 +1488,8 @@ __global__ __launch_bounds__(kBlock) void k_selftest_math(const double* __restri
   out[n + i] = __builtin_sqrt(x);
   out[2 * n + i] = div_cr(x, y);
   out[3 * n + i] = x / y;
+  out[4 * n + i] = inv_mag_unit(x);  // the closed form where every lane of the wave is near 1
+  out[5 * n + i] = 1.0 / (x == 0.0 ? 1.0 : __builtin_sqrt(x));
 }
 
 template <typename T>

@@ -229,14 +229,27 @@ def test_fast_sqrt_div_bit_exact(hip):
     a[:specials.size] = specials
     b[:specials.size] = specials[::-1]
     a[specials.size:2 * specials.size] = np.abs(rng.normal(size=specials.size)) * 1e-8
+    # squared lengths of already-unit vectors: whole waves within 2^-30 of 1 (the closed form), the
+    # range edges, and one wave with a single lane outside (the general path)
+    m = 1 << 16
+    near = 1.0 + np.round(rng.uniform(-2.0 ** 23, 2.0 ** 23, m)) * 2.0 ** -53
+    near[near > 1.0] = 1.0 + np.floor((near[near > 1.0] - 1.0) * 2.0 ** 52) * 2.0 ** -52
+    near[:6] = [1.0, 1.0 - 2.0 ** -30, 1.0 + 2.0 ** -30, 1.0 - 2.0 ** -53, 1.0 + 2.0 ** -52, 1.0 + 2.0 ** -51]
+    near[64 + 17] = 1.5
+    a[1 << 18:(1 << 18) + m] = near
     A = torch.from_numpy(a).cuda()
     Bt = torch.from_numpy(b).cuda()
-    out = torch.empty(4 * n, dtype=torch.float64, device="cuda")
+    out = torch.empty(6 * n, dtype=torch.float64, device="cuda")
     L.check(L.load().rtx_selftest_math(A.data_ptr(), Bt.data_ptr(), n, out.data_ptr(),
                                        torch.cuda.current_stream().cuda_stream), "rtx_selftest_math")
-    o = out.cpu().numpy().reshape(4, n).view(np.uint64)
+    o = out.cpu().numpy().reshape(6, n).view(np.uint64)
     assert np.array_equal(o[0], o[1]), "fast sqrt != full sqrt"
     assert np.array_equal(o[2], o[3]), "fast div != full div"
+    pos = a >= 0
+    assert np.array_equal(o[4][pos], o[5][pos]), "unit renormalisation != 1 / sqrt"
+    with np.errstate(all="ignore"):
+        want = 1.0 / np.where(a == 0, 1.0, np.sqrt(np.where(pos, a, 0.0)))
+    assert np.array_equal(o[5][pos], want[pos].view(np.uint64))
     with np.errstate(all="ignore"):
         pos = a >= 0
         assert np.array_equal(o[1][pos], np.sqrt(a[pos]).view(np.uint64))
