@@ -874,6 +874,7 @@ __device__ __forceinline__ void reflect_dir(double& dx, double& dy, double& dz, 
 // ------------------------------------------------------------------------------------------
 
 __device__ __forceinline__ int global_row(const Params& p, int lr) {
+  if (p.n_parts == 1) return lr;  // a whole frame (uniform branch: no integer divisions)
   return ((lr / p.row_block) * p.n_parts + p.part) * p.row_block + (lr % p.row_block);
 }
 
@@ -894,15 +895,20 @@ __device__ __forceinline__ void camera_dir(const cdouble* sc, int col, int r, in
   dz = vz * rr;
 }
 
+// the camera ray of pixel (col, local row lr) of the launch's tile
+__device__ __forceinline__ void camera_ray(const Params& p, int col, int lr, double& ox, double& oy, double& oz,
+                                           double& dx, double& dy, double& dz) {
+  const cdouble* sc = (const cdouble*)p.scene;
+  camera_dir(sc, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
+  ox = sc[RTX_H_CAM + 0];
+  oy = sc[RTX_H_CAM + 1];
+  oz = sc[RTX_H_CAM + 2];
+}
+
 __device__ __forceinline__ void load_ray(const Params& p, int64_t i, double& ox, double& oy, double& oz, double& dx,
                                          double& dy, double& dz) {
-  const cdouble* sc = (const cdouble*)p.scene;
   if (p.mode == 0) {
-    const int lr = (int)(i / p.width), col = (int)(i % p.width);
-    camera_dir(sc, col, global_row(p, lr), p.width, p.height, dx, dy, dz);
-    ox = sc[RTX_H_CAM + 0];
-    oy = sc[RTX_H_CAM + 1];
-    oz = sc[RTX_H_CAM + 2];
+    camera_ray(p, (int)(i % p.width), (int)(i / p.width), ox, oy, oz, dx, dy, dz);
   } else {
     const int64_t n = p.n;
     dx = p.dir[i];
@@ -971,12 +977,13 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   bool active;
   int kb = 0;                  // absolute level of this launch's first ray (mode 2: the resumed level)
   const double* rin = nullptr;  // mode 2: the chain's resume record (levels 0..kb-1)
+  int col = 0, lr = 0;         // mode 0: the pixel's column and local row
   if (p.mode == 0) {
     // kWavesX x kWavesY waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
     // (wave_tile: (bx, by) is this wave's own kWaveW x kWaveH tile)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = wave_tile ? bx * kWaveW + (lane % kWaveW) : bx * kTileW + (w % kWavesX) * kWaveW + (lane % kWaveW);
-    const int lr = wave_tile ? by * kWaveH + (lane / kWaveW) : by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
+    col = wave_tile ? bx * kWaveW + (lane % kWaveW) : bx * kTileW + (w % kWavesX) * kWaveW + (lane % kWaveW);
+    lr = wave_tile ? by * kWaveH + (lane / kWaveW) : by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else if (!DEEP || p.mode == 1) {
@@ -1014,6 +1021,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (rin) {
       ox = rin[0]; oy = rin[1]; oz = rin[2];
       dx = rin[3]; dy = rin[4]; dz = rin[5];
+    } else if (cam0) {
+      camera_ray(p, col, lr, ox, oy, oz, dx, dy, dz);  // no division of the pixel index
     } else {
       load_ray(p, i, ox, oy, oz, dx, dy, dz);
     }
