@@ -30,8 +30,9 @@
  *  - Scene blob: float64 array built by the host packer (scene_pack.py), layout below. It holds
  *    everything the reference reads from Scene3D during a render.
  *  - Arithmetic is IEEE float64 with no contraction (built with -ffp-contract=off), in the
- *    reference's operation order; sin and pow are the only non-correctly-rounded operations
- *    (≈1 ulp, as NumPy's SIMD versions are).
+ *    reference's operation order; sin (<= 2 ulp) and pow (x^5, x^2.5 by multiplications and a
+ *    square root) are the only operations that are not correctly rounded, as NumPy's SIMD sin and
+ *    pow (~1 ulp) are not either.
  */
 #ifndef RTX_HIP_H
 #define RTX_HIP_H

@@ -660,6 +660,37 @@ __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, d
 
 // (x)^5 and (x)^2.5 for x in [0, 1] (shader.py:291, :310). NumPy evaluates these with its SIMD pow;
 // both are ~1 ulp, not correctly rounded, so neither side is "exact" here.
+// np.sin (shader.py:211) for |x| <= 2^20. Neither side is correctly rounded (NumPy's SIMD sin is
+// ~1 ulp); this one is <= 2 ulp (tests/test_sin.py: 1.9 ulp measured against long-double sin).
+// x - n*pi with n = rint(x/pi): the first fma is exact (x and n*P1 are multiples of 2^-52 and
+// their difference is below 2), the next two add the rest of pi to ~160 bits. Then
+// sin(r) = r + r^3 * p(r^2) on [-pi/2, pi/2] with the Taylor coefficients up to r^21 (truncation
+// 1.2e-18 relative), and sin(x) = (-1)^n sin(r).
+__device__ __forceinline__ double sin_reduced(double x) {
+  const double n = __builtin_rint(x * 0x1.45f306dc9c883p-2);
+  double r = __builtin_fma(-n, 0x1.921fb54442d18p+1, x);
+  r = __builtin_fma(-n, 0x1.1a62633145c07p-53, r);
+  r = __builtin_fma(-n, -0x1.f1976b7ed8fbcp-109, r);
+  const double z = r * r;
+  double q = 0x1.71b8ef6dcf572p-66;  // 1/21!
+  q = __builtin_fma(z, q, -0x1.2f49b46814157p-57);
+  q = __builtin_fma(z, q, 0x1.952c77030ad4ap-49);
+  q = __builtin_fma(z, q, -0x1.ae7f3e733b81fp-41);
+  q = __builtin_fma(z, q, 0x1.6124613a86d09p-33);
+  q = __builtin_fma(z, q, -0x1.ae64567f544e4p-26);
+  q = __builtin_fma(z, q, 0x1.71de3a556c734p-19);
+  q = __builtin_fma(z, q, -0x1.a01a01a01a01ap-13);
+  q = __builtin_fma(z, q, 0x1.1111111111111p-7);
+  q = __builtin_fma(z, q, -0x1.5555555555555p-3);  // -1/3!
+  const double s = __builtin_fma(r * z, q, r);
+  return ((int)n & 1) ? -s : s;
+}
+__device__ __forceinline__ double sin_ref(double x) {
+  // wave-uniform: the reduction above unless some active lane is out of its range (or NaN / inf)
+  if (__ballot(!(fabs(x) <= 0x1.0p20)) == 0) return sin_reduced(x);
+  return sin(x);
+}
+
 __device__ __forceinline__ double pow5(double x) {
   const double x2 = x * x;
   return (x2 * x2) * x;
@@ -744,7 +775,7 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 #ifdef RTX_ABL_SIN  // timing ablation only (wrong output)
     const double ip = phase * 0.1;
 #else
-    const double ip = sin(phase);  // :211
+    const double ip = sin_ref(phase);  // :211
 #endif
     const double hs = mh[RTX_M_HS], omhs = mh[RTX_M_1MHS];
     const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
