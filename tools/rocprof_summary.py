@@ -1,0 +1,35 @@
+"""Per-launch k_render_fast durations from a rocprofv3 --kernel-trace run of bench.py, split into
+warm-up, timed region and the bench's extra launches (the counter launch and the output-path
+renders), to compare with the bench line's live ``roofline.kernel_ms``.
+
+    python tools/rocprof_summary.py gpurun_out/<tag>/prof --warmup 10 --steps 100
+"""
+
+import argparse
+import csv
+import statistics
+from pathlib import Path
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--kernel", default="k_render_fast")
+    a = ap.parse_args()
+    rows = [r for r in csv.DictReader(open(Path(a.prof_dir) / "run_kernel_trace.csv")) if a.kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+    timed = d[a.warmup:a.warmup + a.steps]
+    print(f"kernel {rows[0]['Kernel_Name']}")
+    print(f"launches: {len(d)} (warm-up {a.warmup}, timed {len(timed)}, after {len(d) - a.warmup - len(timed)})")
+    print(f"timed region: mean {statistics.mean(timed):.2f} us, median {statistics.median(timed):.2f} us, "
+          f"min {min(timed):.2f}, max {max(timed):.2f}")
+    print(f"all launches: mean {statistics.mean(d):.2f} us (includes the cold first launch and the counter launch)")
+    print("warm-up:", [round(x, 1) for x in d[:a.warmup]])
+    print("after the timed region:", [round(x, 1) for x in d[a.warmup + a.steps:]])
+
+
+if __name__ == "__main__":
+    main()
