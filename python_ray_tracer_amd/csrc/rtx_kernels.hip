@@ -84,6 +84,18 @@ constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this siz
 #define RTX_DEEP_WORKERS 16384
 #endif
 constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
+#ifndef RTX_LEVELS_IN_LDS
+#define RTX_LEVELS_IN_LDS 1  // capped kernels with B <= RTX_LEVELS_LDS_MAXB keep their levels' colour inputs in LDS
+#endif
+#ifndef RTX_LEVELS_LDS_MAXB
+#define RTX_LEVELS_LDS_MAXB 3
+#endif
+// The colour inputs of the non-terminal levels (4 doubles + the key per level and lane) go to LDS
+// slots indexed by the level instead of a register shift register (no moves per level, 27 fewer
+// live VGPRs): [B][4][kFastBlock] doubles + [B][kFastBlock] ints after the scene table.
+template <int B, bool LDS, bool DEEP>
+constexpr bool levels_in_lds() { return RTX_LEVELS_IN_LDS && LDS && !DEEP && B > 0 && B <= RTX_LEVELS_LDS_MAXB; }
+__host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)B * kFastBlock * (4 * 8 + 4); }
 constexpr int kDeepWorkers = RTX_DEEP_WORKERS;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
@@ -1081,10 +1093,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   }
   if (!active) return;
 
-  // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level)
+  // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level), or,
+  // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
+  constexpr bool LV = levels_in_lds<B, LDS, DEEP>();
   constexpr int NS = B > 0 ? B : 1;
-  double sDli[NS], sDi[NS], sSpec[NS], sVa[NS];
-  int sKey[NS];  // hit sphere | checker bit << 16
+  double sDli[LV ? 1 : NS], sDi[LV ? 1 : NS], sSpec[LV ? 1 : NS], sVa[LV ? 1 : NS];
+  int sKey[LV ? 1 : NS];  // hit sphere | checker bit << 16
+  double* const lvd = LV ? const_cast<double*>(lds_tab) + nsph * kSphWords : nullptr;  // [NS][4][kFastBlock]
+  int* const lvk = LV ? (int*)(lvd + NS * 4 * kFastBlock) : nullptr;                  // [NS][kFastBlock]
+  const int lt = threadIdx.x;
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
   bool deferred = false, appended = false;
@@ -1148,13 +1165,19 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       break;
     }
     // push this level's colour inputs; the reflected ray becomes the next level
+    if constexpr (LV) {
+      double* const l = lvd + (depth * 4) * kFastBlock + lt;
+      l[0] = s.dli; l[kFastBlock] = s.di; l[2 * kFastBlock] = s.spec; l[3 * kFastBlock] = s.va;
+      lvk[depth * kFastBlock + lt] = hit | (s.chk ? 0x10000 : 0);
+    } else {
 #pragma unroll
-    for (int j = NS - 1; j > 0; --j) {
-      sDli[j] = sDli[j - 1]; sDi[j] = sDi[j - 1]; sSpec[j] = sSpec[j - 1]; sVa[j] = sVa[j - 1];
-      sKey[j] = sKey[j - 1];
+      for (int j = NS - 1; j > 0; --j) {
+        sDli[j] = sDli[j - 1]; sDi[j] = sDi[j - 1]; sSpec[j] = sSpec[j - 1]; sVa[j] = sVa[j - 1];
+        sKey[j] = sKey[j - 1];
+      }
+      sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
+      sKey[0] = hit | (s.chk ? 0x10000 : 0);
     }
-    sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
-    sKey[0] = hit | (s.chk ? 0x10000 : 0);
     ++depth;
     reflect_dir(dx, dy, dz, s.nx, s.ny, s.nz);
     ox = s.qx;
@@ -1182,14 +1205,23 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   // fold back (shader.py:106-110): col_k = ((A_k + (spec_k + col_{k+1}*0.5) * g_k) + I_k); the
   // stored levels were lit with g != 0
   const double* mtab = (LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS) + nsph * RTX_GEOM_WORDS;
-  for (int d = 0; d < depth; ++d) {
-    const int key = sKey[0];
-    hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true, sSpec[0],
-              sVa[0], cr, cg, cb, cr, cg, cb);
+  if constexpr (LV) {
+    for (int d = depth - 1; d >= 0; --d) {
+      const double* const l = lvd + (d * 4) * kFastBlock + lt;
+      const int key = lvk[d * kFastBlock + lt];
+      hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, l[0], l[kFastBlock], (key >> 16) != 0, true, true,
+                l[2 * kFastBlock], l[3 * kFastBlock], cr, cg, cb, cr, cg, cb);
+    }
+  } else {
+    for (int d = 0; d < depth; ++d) {
+      const int key = sKey[0];
+      hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true, sSpec[0],
+                sVa[0], cr, cg, cb, cr, cg, cb);
 #pragma unroll
-    for (int j = 0; j < NS - 1; ++j) {
-      sDli[j] = sDli[j + 1]; sDi[j] = sDi[j + 1]; sSpec[j] = sSpec[j + 1]; sVa[j] = sVa[j + 1];
-      sKey[j] = sKey[j + 1];
+      for (int j = 0; j < NS - 1; ++j) {
+        sDli[j] = sDli[j + 1]; sDi[j] = sDi[j + 1]; sSpec[j] = sSpec[j + 1]; sVa[j] = sVa[j + 1];
+        sKey[j] = sKey[j + 1];
+      }
     }
   }
   if constexpr (DEEP) {  // a continued chain: fold on through the levels of its record (same fold)
@@ -1684,7 +1716,8 @@ template <int B, bool DEEP = false>
 void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
   Params p = p0;
   if (p.nsph <= kLdsMaxSpheres) {
-    const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double);
+    const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
+                       (levels_in_lds<B, true, DEEP>() ? level_lds_bytes(B) : 0);
     if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP>, lds, p);
     hipLaunchKernelGGL((k_render_fast<B, true, DEEP>), grid, dim3(kFastBlock), lds, s, p);
   } else {
