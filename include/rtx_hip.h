@@ -167,7 +167,8 @@ enum {
   RTX_WS_COUNT = 0,    /* uint32: deferred rays            */
   RTX_WS_STATUS = 1,   /* uint32: RTX_ST_* flags           */
   RTX_WS_DONE = 2,     /* uint32: finished blocks of the general kernel (reset by the last one) */
-  RTX_WS_COUNT2 = 3,   /* uint32: rays deferred by the continuation pass (caps above 8 or none) */
+  RTX_WS_COUNT2 = 3,   /* uint32: rays deferred by the first continuation pass (caps above 8 or none) */
+  RTX_WS_COUNT3 = 4,   /* uint32: rays deferred by the second continuation pass */
   RTX_WS_HDR_BYTES = 256
 };
 enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2 };

@@ -140,7 +140,8 @@ struct Params {
   const uint32_t* in_count;
   const double* in_rec;
   int in_level;
-  int64_t rec_cap;
+  int64_t rec_cap;     // records drec holds
+  int64_t in_rec_cap;  // records in_rec holds
   double* stack;
   int64_t n_workers;
   int stack_levels;
@@ -159,9 +160,10 @@ struct Params {
 // Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
 // (hits counted through level b) + 1 << 60. The general kernel re-renders the pixel from level 0
 // and skips the per-level counts the fast kernel already made (a, b = -1: none).
-constexpr int kFrameShift = 40;
-constexpr int kRaysShift = 56;
-constexpr int kHitsShift = 60;
+constexpr int kFrameShift = 34;
+constexpr int kRaysShift = 50;
+constexpr int kHitsShift = 57;
+constexpr int kLevelMask = 0x7F;  // 7-bit level fields (level + 1)
 // Resume record of a pixel deferred for depth at level L = RTX_DEEP_LEVELS: the next level's ray
 // (origin, direction) and the colour inputs (dli, di, spec, va, key) of levels 0..L; the general
 // kernel continues the chain at level L + 1 instead of re-rendering it from level 0.
@@ -171,8 +173,9 @@ constexpr int kHitsShift = 60;
 #endif
 constexpr int kRecLevelWords = 5;
 __host__ __device__ constexpr int rec_words(int level) { return 6 + kRecLevelWords * (level + 1); }
-constexpr int kDeepLevel2 = 2 * RTX_DEEP_LEVELS + 1;  // deferral level of the continuation pass
-static_assert(kDeepLevel2 + 1 < 16, "deferred-entry level fields hold 4 bits");
+constexpr int kDeepLevel2 = 2 * RTX_DEEP_LEVELS + 1;  // deferral level of the first continuation pass
+constexpr int kDeepLevel3 = 3 * RTX_DEEP_LEVELS + 2;  // ... and of the second
+static_assert(kDeepLevel3 + 2 < kLevelMask, "deferred-entry level fields hold 7 bits");
 constexpr int64_t kMaxRecords = int64_t(1) << 18;
 
 // append one entry to the launch's deferred list; returns its slot (or -1 when the list is full)
@@ -1038,8 +1041,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (active) {
       const uint64_t e = p.in_list[item];
       i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
-      const int rt = (int)((e >> kRaysShift) & 0xF) - 1, ht = (int)((e >> kHitsShift) & 0xF) - 1;
-      if (rt == p.in_level && ht == rt && item < p.rec_cap) {
+      const int rt = (int)((e >> kRaysShift) & kLevelMask) - 1, ht = (int)((e >> kHitsShift) & kLevelMask) - 1;
+      if (rt == p.in_level && ht == rt && item < p.in_rec_cap) {
         rin = p.in_rec + item * rec_words(p.in_level);
         kb = rt + 1;
       } else {  // a tie, or a chain without a record: on to the general kernel unchanged
@@ -1485,8 +1488,8 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
       const uint64_t e = list[item];
       const int64_t i = (int64_t)(e & ((uint64_t(1) << kFrameShift) - 1));
       const int f = (int)((e >> kFrameShift) & 0xFFFF);
-      const int rays_through = (int)((e >> kRaysShift) & 0xF) - 1;
-      const int hits_through = (int)((e >> kHitsShift) & 0xF) - 1;
+      const int rays_through = (int)((e >> kRaysShift) & kLevelMask) - 1;
+      const int hits_through = (int)((e >> kHitsShift) & kLevelMask) - 1;
       // The scene is read through the scalar cache (wave-uniform pointers) while a wave's lanes may
       // hold rays of different frames of a multi-frame launch: lanes sharing the first active
       // lane's frame run together, then the next frame (a waterfall over the wave's frames).
@@ -1497,7 +1500,7 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
           // a chain deferred for depth (rays and hits counted through the same level) resumes from
           // its record when it has one
           const bool resume = p.in_rec && rays_through == p.in_level && hits_through == rays_through &&
-                              item < p.rec_cap;
+                              item < p.in_rec_cap;
           double ox = 0.0, oy = 0.0, oz = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
           if (!resume) load_ray(q, i, ox, oy, oz, dx, dy, dz);
           double cr, cg, cb;
@@ -1516,9 +1519,11 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
     if (gridDim.x == 1) {  // one block: no other reader of the counters
       hdr[RTX_WS_COUNT] = 0u;
       hdr[RTX_WS_COUNT2] = 0u;
+      hdr[RTX_WS_COUNT3] = 0u;
     } else if (atomicAdd(hdr + RTX_WS_DONE, 1u) == gridDim.x - 1) {
       hdr[RTX_WS_COUNT] = 0u;
       hdr[RTX_WS_COUNT2] = 0u;
+      hdr[RTX_WS_COUNT3] = 0u;
       hdr[RTX_WS_DONE] = 0u;
     }
   }
@@ -1666,23 +1671,31 @@ int64_t records_for(int64_t n, int max_bounces) {  // resume records: only when 
   const bool capped = max_bounces >= 0 && max_bounces <= RTX_CAPPED_MAX;
   return capped ? 0 : (n < kMaxRecords ? n : kMaxRecords);
 }
+// records of the second continuation pass (chains alive after level kDeepLevel2 are rare)
+int64_t records3_for(int64_t n, int max_bounces) {
+  const int64_t r = records_for(n, max_bounces);
+  return r < (kMaxRecords >> 2) ? r : (kMaxRecords >> 2);
+}
 
 size_t round256(size_t b) { return (b + 255) / 256 * 256; }
 
-// Workspace: header | tile counters | list 1 | (deep chains:) list 2 | records of level RTX_DEEP_LEVELS | records of
-// level kDeepLevel2 | general-kernel stacks
+// Workspace: header | tile counters | list 1 | (deep chains:) lists 2 and 3 | records of level
+// RTX_DEEP_LEVELS, kDeepLevel2 and kDeepLevel3 | general-kernel stacks
 struct WsLayout {
-  size_t fetch, list1, list2, rec1, rec2, stack, total;
+  size_t fetch, list1, list2, list3, rec1, rec2, rec3, stack, total;
 };
 WsLayout ws_layout(int64_t n, int max_bounces) {
   WsLayout w{};
   const int64_t nrec = records_for(n, max_bounces);
+  const int64_t nrec3 = records3_for(n, max_bounces);
   w.fetch = RTX_WS_HDR_BYTES;
   w.list1 = w.fetch + (size_t)kMaxFetch * kFetchStride * sizeof(uint32_t);
   w.list2 = w.list1 + round256(list_bytes(n));
-  w.rec1 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
+  w.list3 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
+  w.rec1 = w.list3 + (nrec ? round256(list_bytes(n)) : 0);
   w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(RTX_DEEP_LEVELS) * sizeof(double));
-  w.stack = w.rec2 + round256((size_t)nrec * rec_words(kDeepLevel2) * sizeof(double));
+  w.rec3 = w.rec2 + round256((size_t)nrec * rec_words(kDeepLevel2) * sizeof(double));
+  w.stack = w.rec3 + round256((size_t)nrec3 * rec_words(kDeepLevel3) * sizeof(double));
   w.total = w.stack + (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
   return w;
 }
@@ -1765,6 +1778,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   double* const rec1 = (double*)(p.ws + lay.rec1);
   double* const rec2 = (double*)(p.ws + lay.rec2);
   p.rec_cap = records_for(n_all, p.max_bounces);
+  p.in_rec_cap = p.rec_cap;
   p.stack = (double*)(p.ws + lay.stack);
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
@@ -1810,24 +1824,35 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.in_rec = capped ? nullptr : rec1;
   p.in_level = RTX_DEEP_LEVELS;
   if (!capped && p.n_frames == 1) {
-    // continuation pass: chains deferred for depth go on for RTX_DEEP_LEVELS + 1 more levels in the
-    // register-resident kernel; ties and what is still alive after it go to the general kernel
-    Params q = p;
-    q.mode = 2;
-    q.n_tiles_x = q.n_tiles_y = 0;
-    q.n_fetch = 0;
-    q.dlist = list2;
-    q.dcount = hdr + RTX_WS_COUNT2;
-    q.drec = rec2;
-    q.drec_level = kDeepLevel2;
-    const int64_t tiles = (n_all + kFastBlock - 1) / kFastBlock;
-    const int64_t cap = 4 * (int64_t)device_cus();
-    launch_fast_deep(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
-    if (int e = check_launch("k_render_fast (continuation)")) return e;
-    p.in_list = list2;
-    p.in_count = hdr + RTX_WS_COUNT2;
-    p.in_rec = rec2;
-    p.in_level = kDeepLevel2;
+    // continuation passes: chains deferred for depth go on for RTX_DEEP_LEVELS + 1 more levels in
+    // the register-resident kernel, twice; ties and what is still alive after them go to the
+    // general kernel
+    uint64_t* const lists[2] = {list2, (uint64_t*)(p.ws + lay.list3)};
+    uint32_t* const counts[2] = {hdr + RTX_WS_COUNT2, hdr + RTX_WS_COUNT3};
+    double* const recs[2] = {rec2, (double*)(p.ws + lay.rec3)};
+    const int levels[2] = {kDeepLevel2, kDeepLevel3};
+    const int64_t caps[2] = {p.rec_cap, records3_for(n_all, p.max_bounces)};
+    for (int pass = 0; pass < 2; ++pass) {
+      Params q = p;
+      q.mode = 2;
+      q.n_tiles_x = q.n_tiles_y = 0;
+      q.n_fetch = 0;
+      q.dlist = lists[pass];
+      q.dcount = counts[pass];
+      q.drec = recs[pass];
+      q.drec_level = levels[pass];
+      q.rec_cap = caps[pass];
+      q.in_rec_cap = pass == 0 ? p.rec_cap : caps[0];
+      const int64_t tiles = (n_all + kFastBlock - 1) / kFastBlock;
+      const int64_t cap = 4 * (int64_t)device_cus();
+      launch_fast_deep(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
+      if (int e = check_launch("k_render_fast (continuation)")) return e;
+      p.in_list = lists[pass];
+      p.in_count = counts[pass];
+      p.in_rec = recs[pass];
+      p.in_level = levels[pass];
+      p.in_rec_cap = caps[pass];
+    }
   }
   // deferred rays: ties, and chains longer than the fast kernel's levels
   hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);
