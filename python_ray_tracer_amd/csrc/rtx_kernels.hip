@@ -176,7 +176,17 @@ __host__ __device__ constexpr int rec_words(int level) { return 6 + kRecLevelWor
 constexpr int kDeepLevel2 = 2 * RTX_DEEP_LEVELS + 1;  // deferral level of the first continuation pass
 constexpr int kDeepLevel3 = 3 * RTX_DEEP_LEVELS + 2;  // ... and of the second
 static_assert(kDeepLevel3 + 2 < kLevelMask, "deferred-entry level fields hold 7 bits");
-constexpr int64_t kMaxRecords = int64_t(1) << 18;
+// Resume-record capacities per deferral level (pass 0: the first pass's level RTX_DEEP_LEVELS;
+// 1, 2: the continuation passes'): at least 2^18 / 2^16 / 2^14, or one per 32 / 256 / 2048 pixels,
+// whichever is more. Chains alive at level 5 are 0.2-1.4% of the pixels in the bench scenes (C4:
+// 467,657 of 33.2 M), far fewer at 11 and 17. An entry beyond the capacity is re-rendered from
+// level 0 by the general kernel: correct, but slow.
+__host__ __device__ constexpr int64_t records_cap(int64_t n, int pass) {
+  const int64_t lo = int64_t(1) << (18 - 2 * pass);
+  const int64_t by_n = n / (int64_t(32) << (3 * pass));
+  const int64_t want = by_n > lo ? by_n : lo;
+  return n < want ? n : want;
+}
 
 // append one entry to the launch's deferred list; returns its slot (or -1 when the list is full)
 __device__ __forceinline__ int64_t append_deferred(const Params& p, uint64_t entry) {
@@ -1667,14 +1677,10 @@ int64_t workers_for(int64_t n, int max_bounces) {
 
 size_t list_bytes(int64_t n) { return (size_t)n * sizeof(int64_t); }
 
-int64_t records_for(int64_t n, int max_bounces) {  // resume records: only when chains are deferred for depth
+// resume records of deferral pass `pass`: only when chains are deferred for depth
+int64_t records_for(int64_t n, int max_bounces, int pass = 0) {
   const bool capped = max_bounces >= 0 && max_bounces <= RTX_CAPPED_MAX;
-  return capped ? 0 : (n < kMaxRecords ? n : kMaxRecords);
-}
-// records of the second continuation pass (chains alive after level kDeepLevel2 are rare)
-int64_t records3_for(int64_t n, int max_bounces) {
-  const int64_t r = records_for(n, max_bounces);
-  return r < (kMaxRecords >> 2) ? r : (kMaxRecords >> 2);
+  return capped ? 0 : records_cap(n, pass);
 }
 
 size_t round256(size_t b) { return (b + 255) / 256 * 256; }
@@ -1687,14 +1693,15 @@ struct WsLayout {
 WsLayout ws_layout(int64_t n, int max_bounces) {
   WsLayout w{};
   const int64_t nrec = records_for(n, max_bounces);
-  const int64_t nrec3 = records3_for(n, max_bounces);
+  const int64_t nrec2 = records_for(n, max_bounces, 1);
+  const int64_t nrec3 = records_for(n, max_bounces, 2);
   w.fetch = RTX_WS_HDR_BYTES;
   w.list1 = w.fetch + (size_t)kMaxFetch * kFetchStride * sizeof(uint32_t);
   w.list2 = w.list1 + round256(list_bytes(n));
   w.list3 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
   w.rec1 = w.list3 + (nrec ? round256(list_bytes(n)) : 0);
   w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(RTX_DEEP_LEVELS) * sizeof(double));
-  w.rec3 = w.rec2 + round256((size_t)nrec * rec_words(kDeepLevel2) * sizeof(double));
+  w.rec3 = w.rec2 + round256((size_t)nrec2 * rec_words(kDeepLevel2) * sizeof(double));
   w.stack = w.rec3 + round256((size_t)nrec3 * rec_words(kDeepLevel3) * sizeof(double));
   w.total = w.stack + (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
   return w;
@@ -1831,7 +1838,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     uint32_t* const counts[2] = {hdr + RTX_WS_COUNT2, hdr + RTX_WS_COUNT3};
     double* const recs[2] = {rec2, (double*)(p.ws + lay.rec3)};
     const int levels[2] = {kDeepLevel2, kDeepLevel3};
-    const int64_t caps[2] = {p.rec_cap, records3_for(n_all, p.max_bounces)};
+    const int64_t caps[2] = {records_for(n_all, p.max_bounces, 1), records_for(n_all, p.max_bounces, 2)};
     for (int pass = 0; pass < 2; ++pass) {
       Params q = p;
       q.mode = 2;
@@ -1842,7 +1849,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
       q.drec = recs[pass];
       q.drec_level = levels[pass];
       q.rec_cap = caps[pass];
-      q.in_rec_cap = pass == 0 ? p.rec_cap : caps[0];
+      q.in_rec_cap = p.in_rec_cap;
       const int64_t tiles = (n_all + kFastBlock - 1) / kFastBlock;
       const int64_t cap = 4 * (int64_t)device_cus();
       launch_fast_deep(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
