@@ -90,6 +90,9 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
 #ifndef RTX_LEVELS_LDS_MAXB
 #define RTX_LEVELS_LDS_MAXB 3
 #endif
+#ifndef RTX_LV_WAVES
+#define RTX_LV_WAVES 5  // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
+#endif
 // The colour inputs of the non-terminal levels (4 doubles + the key per level and lane) go to LDS
 // slots indexed by the level instead of a register shift register (no moves per level, 27 fewer
 // live VGPRs): [B][4][kFastBlock] doubles + [B][kFastBlock] ints after the scene table.
@@ -1249,7 +1252,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 }
 
 template <int B, bool LDS, bool DEEP>
-__global__ __launch_bounds__(kFastBlock, DEEP ? RTX_DEEP_WAVES : RTX_FAST_WAVES) void k_render_fast(Params p0) {
+__global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : levels_in_lds<B, LDS, DEEP>() ? RTX_LV_WAVES : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
