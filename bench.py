@@ -15,7 +15,7 @@ its interleaved row tile of ONE frame and the tiles are gathered to rank 0 (RCCL
 Timing: W untimed warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
 The dominant kernel's own time is measured live with HIP events recorded by the library on the
 launch stream (rtx_profile_*) around one launch in --prof-every of the timed region, for the
-roofline (an event pair costs ~7 us of stream time, so timing every launch would depress `value`). Rank 0 also times the CPU oracle (NumPy float64,
+roofline (timing a launch costs stream time, so timing every launch would depress `value`). Rank 0 also times the CPU oracle (NumPy float64,
 single core) on a bounded sample of the same workload.
 """
 
@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0: skip)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--prof-every", type=int, default=10,
-                    help="time the dominant kernel with HIP events on one launch in this many (an event pair "
-                         "adds ~7 us of stream time per launch; 1 = every launch)")
+                    help="time the dominant kernel with HIP events on one launch in this many (timing a launch "
+                         "costs stream time; 1 = every launch)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()

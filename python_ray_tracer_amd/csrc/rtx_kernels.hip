@@ -30,6 +30,7 @@
 //                     list of k_render_fast from level 0. Its last block resets the list counter,
 //                     so the workspace is left zeroed for the next call (no per-frame memset).
 //   k_ray_dirs, k_intersect, k_quantize — the remaining boundary functions.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -1611,8 +1612,9 @@ int check_launch(const char* what) {
   return RTX_OK;
 }
 
-// Optional live timing of the dominant kernel (bench.py's roofline): a pool of event pairs recorded
-// on the launch stream around every k_render_fast (or k_render_general when it does all the work).
+// Optional live timing of the dominant kernel (bench.py's roofline): a pool of event pairs handed to
+// the k_render_fast launch itself (hipExtLaunchKernelGGL), so they time the dispatch from its start
+// to its end, as rocprofv3's kernel trace does, without the gap an event recorded before it adds.
 struct Prof {
   int cap = 0;
   int used = 0;
@@ -1630,10 +1632,14 @@ void prof_free() {
   g_prof.every = every;
 }
 
-inline void prof_mark(int which, hipStream_t s) {
-  if (which == 0) g_prof.on = g_prof.cap && g_prof.used < g_prof.cap && g_prof.seen++ % g_prof.every == 0;
-  if (g_prof.on) (void)hipEventRecord(g_prof.ev[2 * g_prof.used + which], s);
+inline void prof_mark(int which, hipStream_t) {
+  // launches every-1, 2*every-1, ...: not the first one after rtx_profile_enable, which follows an
+  // idle GPU in bench.py (barrier + synchronize) and runs a few µs slow
+  if (which == 0)
+    g_prof.on = g_prof.cap && g_prof.used < g_prof.cap && g_prof.seen++ % g_prof.every == g_prof.every - 1;
 }
+// the start / stop event of the launch being timed (null: not timed)
+inline hipEvent_t prof_event(int which) { return g_prof.on ? g_prof.ev[2 * g_prof.used + which] : nullptr; }
 inline void prof_next() {
   if (g_prof.on) ++g_prof.used;
   g_prof.on = false;
@@ -1742,10 +1748,12 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
     const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
                        (levels_in_lds<B, true, DEEP>() ? level_lds_bytes(B) : 0);
     if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP>, lds, p);
-    hipLaunchKernelGGL((k_render_fast<B, true, DEEP>), grid, dim3(kFastBlock), lds, s, p);
+    hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP>), grid, dim3(kFastBlock), (uint32_t)lds, s, prof_event(0),
+                          prof_event(1), 0u, p);
   } else {
     if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP>, 0, p);
-    hipLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0, s, p);
+    hipExtLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0u, s, prof_event(0),
+                          prof_event(1), 0u, p);
   }
 }
 

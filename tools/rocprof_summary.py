@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--kernel", default="k_render_fast")
+    ap.add_argument("--prof-every", type=int, default=10, help="bench.py's sampling stride")
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(Path(a.prof_dir) / "run_kernel_trace.csv")) if a.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -26,6 +27,10 @@ def main():
     print(f"launches: {len(d)} (warm-up {a.warmup}, timed {len(timed)}, after {len(d) - a.warmup - len(timed)})")
     print(f"timed region: mean {statistics.mean(timed):.2f} us, median {statistics.median(timed):.2f} us, "
           f"min {min(timed):.2f}, max {max(timed):.2f}")
+    e = a.prof_every
+    samp = [timed[k] for k in range(e - 1, len(timed), e)]
+    print(f"launches bench.py times live ({e - 1}, {2 * e - 1}, ... of the timed region): mean "
+          f"{statistics.mean(samp):.2f} us over {len(samp)}")
     print(f"all launches: mean {statistics.mean(d):.2f} us (includes the cold first launch and the counter launch)")
     print("warm-up:", [round(x, 1) for x in d[:a.warmup]])
     print("after the timed region:", [round(x, 1) for x in d[a.warmup + a.steps:]])
