@@ -89,7 +89,10 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
 #define RTX_LEVELS_IN_LDS 1  // capped kernels with B <= RTX_LEVELS_LDS_MAXB keep their levels' colour inputs in LDS
 #endif
 #ifndef RTX_LEVELS_LDS_MAXB
-#define RTX_LEVELS_LDS_MAXB 3
+#define RTX_LEVELS_LDS_MAXB 4  // the deepest cap with LDS level slots
+#endif
+#ifndef RTX_LEVELS_LDS_SLOTS
+#define RTX_LEVELS_LDS_SLOTS 3  // levels kept in LDS; deeper ones (B = 4) in a register slot
 #endif
 #ifndef RTX_LV_WAVES
 #define RTX_LV_WAVES 5  // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
@@ -99,7 +102,8 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
 // live VGPRs): [B][4][kFastBlock] doubles + [B][kFastBlock] ints after the scene table.
 template <int B, bool LDS, bool DEEP>
 constexpr bool levels_in_lds() { return RTX_LEVELS_IN_LDS && LDS && !DEEP && B > 0 && B <= RTX_LEVELS_LDS_MAXB; }
-__host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)B * kFastBlock * (4 * 8 + 4); }
+__host__ __device__ constexpr int level_lds_slots(int B) { return B < RTX_LEVELS_LDS_SLOTS ? B : RTX_LEVELS_LDS_SLOTS; }
+__host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)level_lds_slots(B) * kFastBlock * (4 * 8 + 4); }
 constexpr int kDeepWorkers = RTX_DEEP_WORKERS;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
@@ -1114,10 +1118,13 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
   constexpr bool LV = levels_in_lds<B, LDS, DEEP>();
   constexpr int NS = B > 0 ? B : 1;
-  double sDli[LV ? 1 : NS], sDi[LV ? 1 : NS], sSpec[LV ? 1 : NS], sVa[LV ? 1 : NS];
-  int sKey[LV ? 1 : NS];  // hit sphere | checker bit << 16
-  double* const lvd = LV ? const_cast<double*>(lds_tab) + nsph * kSphWords : nullptr;  // [NS][4][kFastBlock]
-  int* const lvk = LV ? (int*)(lvd + NS * 4 * kFastBlock) : nullptr;                  // [NS][kFastBlock]
+  constexpr int NL = LV ? level_lds_slots(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
+  constexpr int NR = LV ? (B > NL ? B - NL : 1) : NS;
+  static_assert(!LV || B - NL <= 1, "one register level beside the LDS slots");
+  double sDli[NR], sDi[NR], sSpec[NR], sVa[NR];
+  int sKey[NR];  // hit sphere | checker bit << 16
+  double* const lvd = LV ? const_cast<double*>(lds_tab) + nsph * kSphWords : nullptr;  // [NL][4][kFastBlock]
+  int* const lvk = LV ? (int*)(lvd + NL * 4 * kFastBlock) : nullptr;                  // [NL][kFastBlock]
   const int lt = threadIdx.x;
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
@@ -1183,9 +1190,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     // push this level's colour inputs; the reflected ray becomes the next level
     if constexpr (LV) {
-      double* const l = lvd + (depth * 4) * kFastBlock + lt;
-      l[0] = s.dli; l[kFastBlock] = s.di; l[2 * kFastBlock] = s.spec; l[3 * kFastBlock] = s.va;
-      lvk[depth * kFastBlock + lt] = hit | (s.chk ? 0x10000 : 0);
+      if (NL == B || k < NL) {  // k: wave-uniform, == depth of every active lane
+        double* const l = lvd + (depth * 4) * kFastBlock + lt;
+        l[0] = s.dli; l[kFastBlock] = s.di; l[2 * kFastBlock] = s.spec; l[3 * kFastBlock] = s.va;
+        lvk[depth * kFastBlock + lt] = hit | (s.chk ? 0x10000 : 0);
+      } else {  // the level beyond the LDS slots
+        sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
+        sKey[0] = hit | (s.chk ? 0x10000 : 0);
+      }
     } else {
 #pragma unroll
       for (int j = NS - 1; j > 0; --j) {
@@ -1223,7 +1235,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   // stored levels were lit with g != 0
   const double* mtab = (LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS) + nsph * RTX_GEOM_WORDS;
   if constexpr (LV) {
-    for (int d = depth - 1; d >= 0; --d) {
+    if constexpr (NL < B) {
+      if (depth > NL) {  // the register level first (the deepest)
+        const int key = sKey[0];
+        hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true,
+                  sSpec[0], sVa[0], cr, cg, cb, cr, cg, cb);
+      }
+    }
+    for (int d = (depth < NL ? depth : NL) - 1; d >= 0; --d) {
       const double* const l = lvd + (d * 4) * kFastBlock + lt;
       const int key = lvk[d * kFastBlock + lt];
       hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, l[0], l[kFastBlock], (key >> 16) != 0, true, true,
