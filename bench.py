@@ -128,7 +128,9 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    L.profile_sample(max(1, args.prof_every))
+    # the library times launches every-1, 2*every-1, ...: at least one of the timed region
+    every = max(1, min(args.prof_every, args.steps))
+    L.profile_sample(every)
     L.profile_enable(args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -225,7 +227,7 @@ def main():
                         "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "alg_bytes_per_launch": alg_bytes},
                 "note": "FP64 VALU-bound megakernel (no dense contraction, no MFMA); achieved = algorithmic "
                         "FLOPs (SURVEY.md 8d model, kernel counters) / kernel time (HIP events on the launch "
-                        f"stream around 1 in {max(1, args.prof_every)} launches of the timed region)",
+                        f"stream around 1 in {every} launches of the timed region)",
             },
             "cpu_baseline": cpu,
             "output_path": out_path,
