@@ -102,8 +102,14 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
 // live VGPRs): [B][4][kFastBlock] doubles + [B][kFastBlock] ints after the scene table.
 template <int B, bool LDS, bool DEEP>
 constexpr bool levels_in_lds() { return RTX_LEVELS_IN_LDS && LDS && !DEEP && B > 0 && B <= RTX_LEVELS_LDS_MAXB; }
-__host__ __device__ constexpr int level_lds_slots(int B) { return B < RTX_LEVELS_LDS_SLOTS ? B : RTX_LEVELS_LDS_SLOTS; }
-__host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)level_lds_slots(B) * kFastBlock * (4 * 8 + 4); }
+// the DEEP variant (3 waves/SIMD: 3 blocks per CU) keeps all its levels in LDS
+template <bool DEEP = false>
+__host__ __device__ constexpr int level_lds_slots(int B) { return DEEP || B < RTX_LEVELS_LDS_SLOTS ? B : RTX_LEVELS_LDS_SLOTS; }
+template <bool DEEP = false>
+__host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)level_lds_slots<DEEP>(B) * kFastBlock * (4 * 8 + 4); }
+#ifndef RTX_DEEP_LV_MAX_SPHERES
+#define RTX_DEEP_LV_MAX_SPHERES 32  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
+#endif
 constexpr int kDeepWorkers = RTX_DEEP_WORKERS;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
@@ -1030,7 +1036,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // overlaps the LDS staging of the scene table. DEEP (caps above 8 or none): chains still alive
 // after B levels are deferred with a resume record, and the continuation mode exists; the capped
 // instantiations compile none of it.
-template <int B, bool LDS, bool DEEP>
+template <int B, bool LDS, bool DEEP, bool LVL>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   const cdouble* sc = (const cdouble*)p.scene;
@@ -1116,9 +1122,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 
   // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level), or,
   // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
-  constexpr bool LV = levels_in_lds<B, LDS, DEEP>();
+  constexpr bool LV = LVL && LDS && B > 0;
   constexpr int NS = B > 0 ? B : 1;
-  constexpr int NL = LV ? level_lds_slots(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
+  constexpr int NL = LV ? level_lds_slots<DEEP>(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
   constexpr int NR = LV ? (B > NL ? B - NL : 1) : NS;
   static_assert(!LV || B - NL <= 1, "one register level beside the LDS slots");
   double sDli[NR], sDi[NR], sSpec[NR], sVa[NR];
@@ -1171,7 +1177,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         for (int w = 0; w < kRecLevelWords * kb; ++w) rec[6 + w] = rin[6 + w];  // levels 0..kb-1
         double* lv = rec + 6 + kRecLevelWords * (kb + B);
         lv[0] = s.dli; lv[1] = s.di; lv[2] = s.spec; lv[3] = s.va; lv[4] = (double)(hit | (s.chk ? 0x10000 : 0));
-        if constexpr (B > 0) {
+        if constexpr (LV) {  // LDS slot d = level kb + d (a DEEP kernel keeps all B levels there)
+          static_assert(!LV || !DEEP || NL == B, "DEEP level slots");
+          for (int d = 0; d < NL; ++d) {
+            const double* const l = lvd + (d * 4) * kFastBlock + lt;
+            double* lj = rec + 6 + kRecLevelWords * (kb + d);
+            lj[0] = l[0]; lj[1] = l[kFastBlock]; lj[2] = l[2 * kFastBlock]; lj[3] = l[3 * kFastBlock];
+            lj[4] = (double)lvk[d * kFastBlock + lt];
+          }
+        } else if constexpr (B > 0) {
 #pragma unroll
           for (int j = 0; j < NS; ++j) {
             double* lj = rec + 6 + kRecLevelWords * (kb + B - 1 - j);
@@ -1271,8 +1285,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   write_out(p, i, cr, cg, cb);
 }
 
-template <int B, bool LDS, bool DEEP>
-__global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : levels_in_lds<B, LDS, DEEP>() ? RTX_LV_WAVES : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
+template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>()>
+__global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? RTX_LV_WAVES : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
@@ -1288,7 +1302,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : levels_in_lds<
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
       for (int64_t t = blockIdx.x; t * kFastBlock < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+        fast_tile<B, LDS, DEEP, LVL>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
     }
@@ -1322,7 +1336,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : levels_in_lds<
 #ifdef RTX_WAVE_TIMES  // per-tile start/end, slot = tile in dispatch order
       const uint64_t ts = __builtin_amdgcn_s_memrealtime();
 #endif
-      fast_tile<B, LDS, DEEP>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
+      fast_tile<B, LDS, DEEP, LVL>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
 #ifdef RTX_WAVE_TIMES
       if (p.stats && lane == 0) {
         p.stats[RTX_S_WORDS + 2 * t] = ts;
@@ -1343,9 +1357,9 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : levels_in_lds<
     // run long bounce chains, while sky rows finish at level 0 and so fill the end of the grid
     // (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on the order.
 #ifdef RTX_FORWARD_ROWS
-    fast_tile<B, LDS, DEEP>(p, blockIdx.x, blockIdx.y, true, lds_tab);
+    fast_tile<B, LDS, DEEP, LVL>(p, blockIdx.x, blockIdx.y, true, lds_tab);
 #else
-    fast_tile<B, LDS, DEEP>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
+    fast_tile<B, LDS, DEEP, LVL>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 #endif
 #ifdef RTX_WAVE_TIMES
     if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1357,7 +1371,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : levels_in_lds<
   const int nt = p.n_tiles_x * p.n_tiles_y;
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
     const int row = t / p.n_tiles_x;
-    fast_tile<B, LDS, DEEP>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, t == (int)blockIdx.x, lds_tab);
+    fast_tile<B, LDS, DEEP, LVL>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, t == (int)blockIdx.x, lds_tab);
   }
 }
 
@@ -1760,15 +1774,27 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
   return dim3((unsigned)blocks);
 }
 
+template <int B, bool DEEP, bool LVL>
+void launch_fast_lds(Params& p, dim3 grid, hipStream_t s) {
+  const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
+  if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL>, lds, p);
+  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL>), grid, dim3(kFastBlock), (uint32_t)lds, s, prof_event(0),
+                        prof_event(1), 0u, p);
+}
+
 template <int B, bool DEEP = false>
 void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
   Params p = p0;
   if (p.nsph <= kLdsMaxSpheres) {
-    const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
-                       (levels_in_lds<B, true, DEEP>() ? level_lds_bytes(B) : 0);
-    if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP>, lds, p);
-    hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP>), grid, dim3(kFastBlock), (uint32_t)lds, s, prof_event(0),
-                          prof_event(1), 0u, p);
+    if constexpr (DEEP) {
+      if (RTX_LEVELS_IN_LDS && p.nsph <= RTX_DEEP_LV_MAX_SPHERES) {
+        launch_fast_lds<B, true, true>(p, grid, s);
+      } else {
+        launch_fast_lds<B, true, false>(p, grid, s);
+      }
+    } else {
+      launch_fast_lds<B, false, levels_in_lds<B, true, false>()>(p, grid, s);
+    }
   } else {
     if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP>, 0, p);
     hipExtLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0u, s, prof_event(0),
