@@ -898,7 +898,9 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
 
   const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));  // :138
   // dome (:239-242): light_direction (0, 1, 0)
-  const double up = ((nx * 0.0) + (ny * 1.0)) + (nz * 0.0);
+  // N.(0, 1, 0) = ((nx*0) + ny*1) + nz*0 is ny itself for finite N (N is finite: P and C are), up to
+  // the sign of a zero, which max0 and the sum below (0.0 + I*(+-0) = +0) erase
+  const double up = ny;
   const int ndome = (int)sc[RTX_H_NDOME];
   double di = 0.0;
   for (int j = 0; j < ndome; ++j) di = di + sc[RTX_H_DOMEI + j] * max0(up);

@@ -354,3 +354,19 @@ def test_large_scene_without_lds_table(hip, B):
     assert np.array_equal(O.to_uint8(got, 72, 40), O.to_uint8(want, 72, 40))
     assert r.stats()["rays"] == st.rays
 
+
+
+@pytest.mark.parametrize("seed", range(14, 22))
+def test_fuzz_scenes_deep_caps(hip, seed):
+    """The fuzz scenes with no cap and caps beyond the fast kernels (the continuation passes, the
+    DEEP kernel's LDS and register variants, the general kernel): colour, uint8 and counters."""
+    spec = _fuzz_spec(seed)
+    B = [None, 12, 20, None][seed % 4]
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL, (seed, np.abs(got - want).max())
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    assert np.array_equal(O.to_uint8(got, W, H), O.to_uint8(want, W, H))
+    s = r.stats()
+    assert s["rays"] == st.rays and s["hits"] == st.hits, seed
