@@ -89,7 +89,13 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
 #define RTX_LEVELS_IN_LDS 1  // capped kernels with B <= RTX_LEVELS_LDS_MAXB keep their levels' colour inputs in LDS
 #endif
 #ifndef RTX_LEVELS_LDS_MAXB
-#define RTX_LEVELS_LDS_MAXB 4  // the deepest cap with LDS level slots
+#define RTX_LEVELS_LDS_MAXB 5  // the deepest cap with LDS level slots
+#endif
+#ifndef RTX_B5_SLOTS
+#define RTX_B5_SLOTS 2  // LDS level slots of the B = 5 kernel (the others in a register shift)
+#endif
+#ifndef RTX_B5_WAVES
+#define RTX_B5_WAVES 4  // its waves/SIMD
 #endif
 #ifndef RTX_LEVELS_LDS_SLOTS
 #define RTX_LEVELS_LDS_SLOTS 3  // levels kept in LDS; deeper ones (B = 4) in a register slot
@@ -104,7 +110,9 @@ template <int B, bool LDS, bool DEEP>
 constexpr bool levels_in_lds() { return RTX_LEVELS_IN_LDS && LDS && !DEEP && B > 0 && B <= RTX_LEVELS_LDS_MAXB; }
 // the DEEP variant (3 waves/SIMD: 3 blocks per CU) keeps all its levels in LDS
 template <bool DEEP = false>
-__host__ __device__ constexpr int level_lds_slots(int B) { return DEEP || B < RTX_LEVELS_LDS_SLOTS ? B : RTX_LEVELS_LDS_SLOTS; }
+__host__ __device__ constexpr int level_lds_slots(int B) {
+  return DEEP || B < RTX_LEVELS_LDS_SLOTS ? B : B >= 5 ? RTX_B5_SLOTS : RTX_LEVELS_LDS_SLOTS;
+}
 template <bool DEEP = false>
 __host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)level_lds_slots<DEEP>(B) * kFastBlock * (4 * 8 + 4); }
 #ifndef RTX_DEEP_LV_MAX_SPHERES
@@ -1128,7 +1136,6 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   constexpr int NS = B > 0 ? B : 1;
   constexpr int NL = LV ? level_lds_slots<DEEP>(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
   constexpr int NR = LV ? (B > NL ? B - NL : 1) : NS;
-  static_assert(!LV || B - NL <= 1, "one register level beside the LDS slots");
   double sDli[NR], sDi[NR], sSpec[NR], sVa[NR];
   int sKey[NR];  // hit sphere | checker bit << 16
   double* const lvd = LV ? const_cast<double*>(lds_tab) + nsph * kSphWords : nullptr;  // [NL][4][kFastBlock]
@@ -1210,7 +1217,12 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         double* const l = lvd + (depth * 4) * kFastBlock + lt;
         l[0] = s.dli; l[kFastBlock] = s.di; l[2 * kFastBlock] = s.spec; l[3 * kFastBlock] = s.va;
         lvk[depth * kFastBlock + lt] = hit | (s.chk ? 0x10000 : 0);
-      } else {  // the level beyond the LDS slots
+      } else {  // levels beyond the LDS slots: a register shift (slot 0 = the most recent)
+#pragma unroll
+        for (int j = NR - 1; j > 0; --j) {
+          sDli[j] = sDli[j - 1]; sDi[j] = sDi[j - 1]; sSpec[j] = sSpec[j - 1]; sVa[j] = sVa[j - 1];
+          sKey[j] = sKey[j - 1];
+        }
         sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
         sKey[0] = hit | (s.chk ? 0x10000 : 0);
       }
@@ -1252,10 +1264,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const double* mtab = (LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS) + nsph * RTX_GEOM_WORDS;
   if constexpr (LV) {
     if constexpr (NL < B) {
-      if (depth > NL) {  // the register level first (the deepest)
+      for (int d = depth - 1; d >= NL; --d) {  // the register levels first (the deepest)
         const int key = sKey[0];
         hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true,
                   sSpec[0], sVa[0], cr, cg, cb, cr, cg, cb);
+#pragma unroll
+        for (int j = 0; j < NR - 1; ++j) {
+          sDli[j] = sDli[j + 1]; sDi[j] = sDi[j + 1]; sSpec[j] = sSpec[j + 1]; sVa[j] = sVa[j + 1];
+          sKey[j] = sKey[j + 1];
+        }
       }
     }
     for (int d = (depth < NL ? depth : NL) - 1; d >= 0; --d) {
@@ -1288,7 +1305,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 }
 
 template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>()>
-__global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? RTX_LV_WAVES : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
+__global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? (B >= 5 ? RTX_B5_WAVES : RTX_LV_WAVES) : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
