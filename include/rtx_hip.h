@@ -143,9 +143,11 @@ enum {
 
 #define RTX_UNBOUNDED (-1)       /* max_bounces: no cap, like the reference recursion */
 #define RTX_UNBOUNDED_LEVELS 333 /* ~ Python's recursion limit / 3 frames per level */
-#define RTX_FAST_MAX_BOUNCES 8   /* bounce caps served entirely by the register-resident kernel; a
+#define RTX_FAST_MAX_BOUNCES 6   /* bounce caps served entirely by the register-resident kernel; a
                                     larger or no cap runs it for a few levels and defers the
-                                    pixels whose chain goes on to the depth-first kernel */
+                                    pixels whose chain goes on to the continuation passes and the
+                                    depth-first kernel (caps 7-8 that way: 1.1-1.6x faster than
+                                    the 7- and 8-level kernels, which spill) */
 
 /* stats buffer (uint64 words, accumulated with atomics; pass NULL to disable) */
 enum {

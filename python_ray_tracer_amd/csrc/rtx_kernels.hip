@@ -1836,12 +1836,10 @@ void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
     case 3: launch_fast_b<3>(p, grid, s); break;
     case 4: launch_fast_b<4>(p, grid, s); break;
     case 5: launch_fast_b<5>(p, grid, s); break;
-    case 6: launch_fast_b<6>(p, grid, s); break;
-    case 7: launch_fast_b<7>(p, grid, s); break;
-    default: launch_fast_b<8>(p, grid, s); break;
+    default: launch_fast_b<6>(p, grid, s); break;
   }
 }
-static_assert(RTX_FAST_MAX_BOUNCES == 8, "launch_fast switch covers 0..8");
+static_assert(RTX_FAST_MAX_BOUNCES == 6, "launch_fast switch covers 0..6");
 
 int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s) {
   if (p.nsph <= 0 || p.nsph > RTX_MAX_SPHERES) return fail(RTX_E_ARG, "n_spheres out of range%s (%lld)", "", p.nsph);

@@ -24,7 +24,7 @@ MAT_WORDS = 24
 MAX_DOMES = 8
 S_WORDS = 264
 WS_HDR_BYTES = 256
-FAST_MAX_BOUNCES = 8
+FAST_MAX_BOUNCES = 6
 UNBOUNDED_LEVELS = 333
 MAX_SPHERES = 1024
 MAGIC = 5527384.0
