@@ -89,7 +89,7 @@ constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
 #define RTX_LEVELS_IN_LDS 1  // capped kernels with B <= RTX_LEVELS_LDS_MAXB keep their levels' colour inputs in LDS
 #endif
 #ifndef RTX_LEVELS_LDS_MAXB
-#define RTX_LEVELS_LDS_MAXB 5  // the deepest cap with LDS level slots
+#define RTX_LEVELS_LDS_MAXB 6  // the deepest cap with LDS level slots
 #endif
 #ifndef RTX_B5_SLOTS
 #define RTX_B5_SLOTS 2  // LDS level slots of the B = 5 kernel (the others in a register shift)
