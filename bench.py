@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--frames-per-step", type=int, default=1,
                     help="frames mode: render this many orbit frames of the config (C5 camera path, "
                          "SURVEY.md 8d) per step in ONE launch (rtx_render_frames)")
+    ap.add_argument("--bounces", type=int, default=None,
+                    help="override the config's bounce cap (-1: unbounded, HipRenderer()'s default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0: skip)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--prof-every", type=int, default=10,
@@ -89,6 +91,8 @@ def main():
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
     spec, B = scenes.CONFIGS[args.config]()
+    if args.bounces is not None:
+        B = None if args.bounces < 0 else args.bounces
     W, H = spec["camera"]["width"], spec["camera"]["height"]
     scene = scenes.build_scene(spec)
     dtype = torch.float64 if args.out == "f64" else torch.float32
@@ -188,8 +192,8 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = px_per_step * args.steps / elapsed / 1e6
         line = {
-            "metric": "Mpixels/sec @1920x1080, 3 reflection bounces" if args.config in ("C2", "C2main")
-            else f"Mpixels/sec ({args.config})",
+            "metric": "Mpixels/sec @1920x1080, 3 reflection bounces" if args.config in ("C2", "C2main") and B == 3
+            else f"Mpixels/sec ({args.config}, {'unbounded' if B is None else B} bounces)",
             "value": round(value, 3),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -207,12 +211,13 @@ def main():
                 "C2main": "main.py scene 1920x1080",
                 "C3": "16 random spheres + checker ground 3840x2160 seed 0",
                 "C4": "64 random spheres + checker ground 7680x4320 seed 0",
-                "C5": "16 random spheres 1920x1080 seed 0"}[args.config] + f", {B} bounces",
+                "C5": "16 random spheres 1920x1080 seed 0"}[args.config]
+                + (", unbounded bounces" if B is None else f", {B} bounces"),
                 "width": W, "height": H, "max_bounces": B, "spheres": S, "output": args.out,
                 "mode": args.mode, "frames_per_step": F, "parallelism": f"{args.mode}x{world}"},
             "roofline": {
                 "bound": "valu",
-                "kernel": f"k_render_fast<{B}>",
+                "kernel": f"k_render_fast<{B}>" if B is not None and B <= 6 else "k_render_fast<5, DEEP> (first pass)",
                 "achieved": round(achieved_tflops, 4),
                 "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s",
