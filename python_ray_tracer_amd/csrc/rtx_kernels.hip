@@ -347,15 +347,17 @@ __device__ __forceinline__ int trunc_parity(double x) {
   return (x == x) && (h != trunc(h));
 }
 
-// b >= 0 and c >= 0 (the sphere lies behind an origin outside it): the reference's root is never
+// b > 0 and c >= 0 (the sphere lies behind an origin outside it): the reference's root is never
 // positive, so the test is FARAWAY without a square root. Proof: disc = fl(fl(b*b) - 4c) <= fl(b*b),
-// and for b >= 0 with b*b finite (b <= 1e150) the correctly rounded sqrt(fl(b*b)) is b itself
-// (b*b*(1 + 2^-53) has a root below b + ulp(b)/2), so sq <= b and s1 = (-b + sq) / 2 <= 0.
+// and for b with b*b a normal double (1e-150 <= b <= 1e150) the correctly rounded sqrt(fl(b*b)) is b
+// itself (b*b*(1 + 2^-53) has a root below b + ulp(b)/2), so sq <= b and s1 = (-b + sq) / 2 <= 0.
+// Below 1e-150, b*b may round up by far more than an ulp in the subnormal range (b = 1.6e-162, c = 0:
+// the reference reports a hit at 3.1e-163, tests/golden/intersect_kat.json), so those take the root.
 __device__ __forceinline__ bool behind(double b, double c) {
 #ifdef RTX_NO_BEHIND
   return false;
 #else
-  return b >= 0.0 && c >= 0.0 && b <= 1e150;
+  return b >= 1e-150 && c >= 0.0 && b <= 1e150;
 #endif
 }
 

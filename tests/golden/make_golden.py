@@ -252,6 +252,9 @@ def main():
     add([0, -99999.5, 0], 99999, [0, 0.2, -2], [0.1, 0.3, 1], "ground sphere, ray upward")
     add([0.55, 0.5, 3], 1.0, [0, 0.2, -2], [0.1, 0.05, 1], "main.py sphere 0")
     add([-0.45, 0.1, 1], 0.4, [0, 0.2, -2], [-0.15, -0.03, 1], "main.py sphere 1")
+    # origin exactly on the surface (c == 0) and b = 1.6e-162 > 0: b*b is subnormal and rounds up,
+    # so sqrt(disc) > b and the far root is a hit at 3.1e-163 (not "behind the origin")
+    add([0, 0, 0], 1, [1, 0, 0], [8e-163, 1, 0], "surface origin, b*b subnormal: tiny hit")
     add([0, 0, 0], 1, [0, 0, -3], [0, 0, 0], "raw")  # zero direction (not normalised)
     (HERE / "intersect_kat.json").write_text(json.dumps(kat, indent=1))
 
