@@ -34,6 +34,34 @@ def main():
     print(f"all launches: mean {statistics.mean(d):.2f} us (includes the cold first launch and the counter launch)")
     print("warm-up:", [round(x, 1) for x in d[:a.warmup]])
     print("after the timed region:", [round(x, 1) for x in d[a.warmup + a.steps:]])
+    timeline(Path(a.prof_dir) / "run_kernel_trace.csv", rows[a.warmup:a.warmup + a.steps])
+
+
+def timeline(csv_path, fast):
+    """Where a step's stream time goes: from one timed k_render_fast start to the next, the fast
+    kernel itself, the other kernels in between, and the idle gaps between kernel boundaries."""
+    allk = sorted(csv.DictReader(open(csv_path)), key=lambda r: int(r["Start_Timestamp"]))
+    spans = {"fast kernel": [], "other kernels": [], "idle gaps": []}
+    names = set()
+    for f0, f1 in zip(fast, fast[1:]):
+        s0, s1 = int(f0["Start_Timestamp"]), int(f1["Start_Timestamp"])
+        inside = [r for r in allk if s0 <= int(r["Start_Timestamp"]) < s1]
+        busy = other = 0
+        end = s0
+        for r in inside:
+            b, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            busy += max(0, min(e, s1) - max(b, end))
+            end = max(end, e)
+            if b != s0:
+                other += e - b
+                names.add(r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")[:50])
+        spans["fast kernel"].append((int(f0["End_Timestamp"]) - s0) / 1e3)
+        spans["other kernels"].append(other / 1e3)
+        spans["idle gaps"].append((s1 - s0 - busy) / 1e3)
+    print(f"step timeline over {len(spans['idle gaps'])} timed steps (start of one fast launch to the next), mean us:")
+    for k, v in spans.items():
+        print(f"  {k:14s} {statistics.mean(v):8.2f}")
+    print("  other kernels:", sorted(names))
 
 
 if __name__ == "__main__":
