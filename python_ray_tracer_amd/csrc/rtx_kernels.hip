@@ -1011,16 +1011,18 @@ __device__ __forceinline__ unsigned char quant_u8(double c) {
 }
 
 __device__ __forceinline__ void write_out(const Params& p, int64_t i, double r, double g, double b) {
+  // the frame is written once and never read back by the kernel: streaming (nontemporal) stores
+  // (A/B, identical output: C5 -1.5..-1.9%, C3 -0.9%, C2 -0.4..-0.8%)
   if (p.out_kind == RTX_OUT_F32_SOA) {
     float* o = (float*)p.out;
-    o[i] = (float)r;
-    o[p.n + i] = (float)g;
-    o[2 * p.n + i] = (float)b;
+    __builtin_nontemporal_store((float)r, o + i);
+    __builtin_nontemporal_store((float)g, o + p.n + i);
+    __builtin_nontemporal_store((float)b, o + 2 * p.n + i);
   } else if (p.out_kind == RTX_OUT_F64_SOA) {
     double* o = (double*)p.out;
-    o[i] = r;
-    o[p.n + i] = g;
-    o[2 * p.n + i] = b;
+    __builtin_nontemporal_store(r, o + i);
+    __builtin_nontemporal_store(g, o + p.n + i);
+    __builtin_nontemporal_store(b, o + 2 * p.n + i);
   } else {
     unsigned char* o = (unsigned char*)p.out + 3 * i;
     o[0] = quant_u8(r);
