@@ -42,9 +42,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2", help="C1|C2|C2main|C3|C4|C5 (python_ray_tracer_amd/scenes.py)")
-    ap.add_argument("--mode", default="frames", choices=["frames", "tiles"])
+    ap.add_argument("--mode", default=None, choices=["frames", "tiles"],
+                    help="default: frames at N=1, tiles (row tiles + RCCL gather of one frame) at N>1")
     ap.add_argument("--row-block", type=int, default=8)
-    ap.add_argument("--out", default="f32", choices=["f32", "f64", "u8"])
+    ap.add_argument("--out", default=None, choices=["f32", "f64", "u8"],
+                    help="frame format left in HBM (default f32; u8 in tiles mode at N>1: the gathered frame is "
+                         "the uint8 image save_image writes)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N>1: skip the extra weak-scaling frames and C4-tiles measurements")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="processes of the row-tiled all-cores CPU baseline (the box's CPU share is 16)")
     ap.add_argument("--frames-per-step", type=int, default=1,
                     help="frames mode: render this many orbit frames of the config (C5 camera path, "
                          "SURVEY.md 8d) per step in ONE launch (rtx_render_frames)")
@@ -62,6 +69,11 @@ def parse():
 
 def main():
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.mode is None:
+        args.mode = "tiles" if world_env > 1 else "frames"
+    if args.out is None:
+        args.out = "u8" if (args.mode == "tiles" and world_env > 1) else "f32"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -114,13 +126,10 @@ def main():
             return r.raytrace_scene(scene.camera.position, r.get_ray_directions(scene.camera), scene)
         px_per_step = W * H * world
     else:
-        from python_ray_tracer_amd.application import render_frame_distributed
-
-        def step():
-            if world == 1:
-                return r.render_tile(scene, out="u8" if args.out == "u8" else None)
-            return render_frame_distributed(scene, r, row_block=args.row_block,
-                                            gather="u8" if args.out == "u8" else "color")
+        # strong scaling: every rank renders its interleaved row tile of ONE frame into a gather
+        # buffer, one gather to rank 0, one device un-permute there; two slots, so the gather of
+        # frame k overlaps the render of frame k+1 (python_ray_tracer_amd/distributed.py)
+        step, drain = tiles_stepper(r, scene, world, args.row_block, "u8" if args.out == "u8" else None)
         px_per_step = W * H
 
     def barrier():  # every rank's queued GPU work done, then all ranks meet
@@ -129,8 +138,13 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    if args.mode != "tiles":
+        def drain():
+            return None
+
     for _ in range(args.warmup):
         step()
+    drain()
     barrier()
     # the library times launches every-1, 2*every-1, ...: at least one of the timed region
     every = max(1, min(args.prof_every, args.steps))
@@ -139,6 +153,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, kern_n = L.profile_collect()
@@ -184,9 +199,17 @@ def main():
 
     out_path = output_path_times(r, scene) if rank == 0 else None
 
+    secondary = None
+    if world > 1 and not args.no_secondary:
+        secondary = secondary_measurements(args, r, spec, B, scene, world, rank, dev, coll_dev, barrier)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(spec, B, args.cpu_seconds)
+        try:
+            cpu = cpu_baseline_all_cores(spec, B, args.cpu_procs, args.cpu_seconds, cpu)
+        except Exception as e:  # noqa: BLE001 - the baseline is reported, never fatal
+            cpu["all_cores_error"] = repr(e)[:300]
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -204,6 +227,7 @@ def main():
             "scaling": "weak" if args.mode == "frames" else "strong",
             "vs_baseline": None,
             "dtype": "f64",
+            "output_dtype": {"f32": "f32 SoA", "f64": "f64 SoA", "u8": "u8 HWC"}[args.out],
             "data": "synthetic",
             "config": {"workload": f"{args.config}: " + {
                 "C1": "README scene 960x540",
@@ -237,8 +261,12 @@ def main():
             "cpu_baseline": cpu,
             "output_path": out_path,
         }
+        if secondary:
+            line["secondary"] = secondary
         if cpu:
             line["gpu_vs_cpu"] = round(value / cpu["value"], 1)
+            if cpu.get("single_core"):
+                line["gpu_vs_cpu_1core"] = round(value / cpu["single_core"]["value"], 1)
         s = json.dumps(line)
         print(s)
         if args.json_out:
@@ -246,6 +274,108 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def tiles_stepper(r, scene, world, row_block, out):
+    """(step, drain) of the strong-scaling tiles mode. World 1: the whole frame rendered into a
+    pre-allocated buffer. World > 1: TileGather with two slots; step k submits frame k and
+    finishes frame k-1 (its gather overlapped frame k's render); drain finishes the last one."""
+    import torch
+
+    if world == 1:
+        W, H = int(scene.camera.width), int(scene.camera.height)
+        buf = (torch.empty((H, W, 3), dtype=torch.uint8, device=r.device) if out == "u8"
+               else torch.empty((3, W * H), dtype=r.color_dtype, device=r.device))
+
+        def step1():
+            return r.render_tile(scene, out=out, into=buf)
+        return step1, (lambda: None)
+    from python_ray_tracer_amd.distributed import TileGather
+
+    tg = TileGather(r, int(scene.camera.width), int(scene.camera.height), row_block=row_block, out=out, slots=2)
+    state = {"k": 0, "open": None}
+
+    def step():
+        slot = state["k"] % 2
+        tg.submit(scene, slot)
+        if state["open"] is not None:
+            tg.finish(state["open"])
+        state["open"] = slot
+        state["k"] += 1
+
+    def drain():
+        if state["open"] is not None:
+            tg.finish(state["open"])
+            state["open"] = None
+    return step, drain
+
+
+def secondary_measurements(args, r, spec, B, scene, world, rank, dev, coll_dev, barrier):
+    """N > 1 extras on the same ranks, each timed like the headline (barrier, K steps, barrier,
+    max over ranks): (1) weak scaling, every rank renders whole frames of the config with no
+    collective (the frame sharding of C5); (2) the C4 scaling config (7680x4320, 65 spheres, B=5)
+    in tiles mode with the uint8 gather."""
+    import torch
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    def timed(step, drain, k, warm):
+        for _ in range(warm):
+            step()
+        drain()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        drain()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    out = {}
+    k = max(10, min(args.steps, 100))
+
+    def frame_step():
+        return r.render_tile(scene, out="u8" if args.out == "u8" else None)
+    t = timed(frame_step, lambda: None, k, 3)
+    out["frames_weak"] = {"value": round(world * W * H * k / t / 1e6, 3), "unit": "Mpixels/s",
+                          "ms_per_step": round(t / k * 1e3, 5), "steps": k, "scaling": "weak",
+                          "config": f"{args.config}, every rank renders whole frames, no collective"}
+    c4spec, c4B = scenes.CONFIGS["C4"]()
+    c4 = scenes.build_scene(c4spec)
+    r4 = HipRenderer(max_bounces=c4B, color_dtype=torch.float32, device=dev)
+    step, drain = tiles_stepper(r4, c4, world, args.row_block, "u8")
+    k4 = 10
+    t = timed(step, drain, k4, 2)
+    out["c4_tiles"] = {"value": round(7680 * 4320 * k4 / t / 1e6, 3), "unit": "Mpixels/s",
+                       "ms_per_step": round(t / k4 * 1e3, 5), "steps": k4, "scaling": "strong",
+                       "config": "C4: 64 random spheres + ground 7680x4320 seed 0, 5 bounces, row tiles "
+                                 f"(row_block {args.row_block}) + gather of the uint8 frame to rank 0"}
+    return out
+
+
+def cpu_baseline_all_cores(spec, B, procs, budget_s, single):
+    """The oracle row-tiled over ``procs`` processes (one core each) through the gloo
+    render_frame_distributed path (oracle/row_tiled.py): render + gather + un-permute of whole
+    frames. ``single``: the 1-core result, kept beside it."""
+    from oracle import row_tiled
+
+    procs = max(1, min(procs, row_tiled.host_cores()))
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    # frames sized to the budget from the single-core time (at least 2)
+    t1 = W * H / (single["value"] * 1e6)
+    frames = int(max(2, min(20, budget_s / max(t1 / procs * 1.5, 1e-3))))
+    res = row_tiled.time_row_tiled(spec, B, procs, frames=frames)
+    best = min(res["times"])
+    return {"value": round(W * H / best / 1e6, 4), "unit": "Mpixels/s", "cores": procs, "kind": "port",
+            "sample": f"{frames} full {W}x{H} frames, B={B}, oracle/numpy_oracle.py row-tiled over {procs} "
+                      f"processes (oracle/row_tiled.py, gloo gather to rank 0), best of {frames} "
+                      f"(median {sorted(res['times'])[len(res['times']) // 2]:.3f}s)",
+            "single_core": single}
 
 
 def output_path_times(r, scene):

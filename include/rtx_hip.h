@@ -173,7 +173,9 @@ enum {
   RTX_WS_COUNT3 = 4,   /* uint32: rays deferred by the second continuation pass */
   RTX_WS_HDR_BYTES = 256
 };
-enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2 };
+/* RTX_ST_BAD_SCENE: the scene blob's magic or sphere count (RTX_H_NSPH) disagrees with the
+ * n_spheres argument; nothing was rendered. */
+enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2, RTX_ST_BAD_SCENE = 4 };
 
 enum {
   RTX_OK = 0,
@@ -233,6 +235,16 @@ int rtx_sphere_intersect(const double* sphere, const double* origins, int64_t or
  * out [n][3] uint8 = (uint8)(255 * clip(c, 0, 1)). */
 int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, void* stream);
 
+/* Frame assembly of the multi-GPU path (render_image_pipeline's row-tile gather, SURVEY.md §8e;
+ * the reference renders one process-local frame, application.py:43-52): `tiles` holds n_parts
+ * gathered row tiles, part p at tiles + p * part_stride_bytes, each as rtx_render_camera wrote it
+ * for (row_block, n_parts, p) with out_kind `kind` (SoA colour: [3][rows_p * width]; u8:
+ * [rows_p][width][3]). Writes the whole frame to `out` in the layout of a whole-frame render
+ * (SoA [3][height * width] or u8 [height][width][3]). part_stride_bytes must hold part 0's tile
+ * (the largest). */
+int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts, int width, int height,
+                      int row_block, int kind, void* out, void* stream);
+
 /* Test hook: out[0:n] = the library's fast-path sqrt(a), out[n:2n] = the compiler's full sqrt(a),
  * out[2n:3n] = fast-path a/b, out[3n:4n] = full a/b, out[4n:5n] = the renormalisation factor of an
  * already-unit vector with |v|^2 = a (closed form when every lane of the wave has a within 2^-30
@@ -246,7 +258,8 @@ int rtx_selftest_math(const double* a, const double* b, int64_t n, double* out, 
  * dispatch itself (hipExtLaunchKernelGGL start/stop events: the kernel's own start and end, as
  * rocprofv3's kernel trace sees them). rtx_profile_collect waits for the recorded events and
  * returns the summed kernel time and the launch count, then resets. rtx_profile_enable(0)
- * disables. Not thread-safe; meant for benchmarks, not for graph capture. */
+ * disables. The profiling state is per calling thread (only that thread's launches are timed);
+ * meant for benchmarks, not for graph capture. */
 int rtx_profile_enable(int max_launches);
 int rtx_profile_collect(double* total_ms, int* n_launches);
 /* Time only one render launch in `every` (default 1: all), the every-th, 2*every-th, ... after

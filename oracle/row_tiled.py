@@ -1,0 +1,103 @@
+"""CPU ORACLE, all host cores — test / baseline infrastructure only, NOT the product path.
+
+The north star asks for the NumPy CPU path "timed on the GPU box's own host cores"; the reference
+itself is single-threaded NumPy. This runs the oracle (``numpy_oracle``, the
+reference's algorithm) row-tiled over P processes through the product's own multi-rank frame path
+(``application.render_frame_distributed`` over gloo): every process renders its interleaved row
+tile with the oracle (one core each), the tiles are gathered to rank 0 and un-permuted there.
+Only ``bench.py``'s ``cpu_baseline`` leg and ``tests/`` use it.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import socket
+import tempfile
+import time
+
+import numpy as np
+
+
+class OracleTileRenderer:
+    """The ``render_tile`` contract of HipRenderer, computed by the oracle on the CPU (float64)."""
+
+    def __init__(self, max_bounces):
+        self.B = max_bounces
+
+    def render_tile(self, scene, row_block, n_parts, part, out=None):
+        import torch
+
+        from oracle import numpy_oracle as O
+        from python_ray_tracer_amd import tiling
+
+        sc = O.scene_from_objects(scene)
+        rows = tiling.tile_rows(sc.height, row_block, n_parts, part)
+        t = O.render_rows(sc, rows, self.B)
+        if out == "u8":
+            return torch.from_numpy(np.ascontiguousarray(O.to_uint8(t, sc.width, len(rows))))
+        return torch.from_numpy(np.ascontiguousarray(t))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, spec, B, frames, outfile, row_block):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.application import render_frame_distributed
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene = scenes.build_scene(spec)
+        r = OracleTileRenderer(B)
+        times = []
+        frame = None
+        for _ in range(frames):
+            dist.barrier()
+            t0 = time.perf_counter()
+            frame = render_frame_distributed(scene, r, row_block=row_block)
+            dist.barrier()  # every rank's tile gathered: the frame is complete on rank 0
+            times.append(time.perf_counter() - t0)
+        if rank == 0:
+            with open(outfile, "w") as f:
+                json.dump({"times": times, "shape": list(frame.shape)}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def time_row_tiled(spec: dict, max_bounces, procs: int, frames: int = 3, row_block: int = 8) -> dict:
+    """Wall time per frame of the row-tiled oracle on ``procs`` processes (one core each):
+    render + gather + un-permute, process start-up and imports excluded. Returns {"times": [...]}."""
+    import torch.multiprocessing as mp
+
+    old = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in old:
+        os.environ[k] = "1"  # one core per process (NumPy's elementwise ufuncs are single-threaded anyway)
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            out = os.path.join(d, "times.json")
+            mp.start_processes(_worker, args=(procs, _free_port(), spec, max_bounces, frames, out, row_block),
+                               nprocs=procs, start_method="spawn", join=True)
+            with open(out) as f:
+                return json.load(f)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def host_cores() -> int:
+    """CPUs this process may run on (the GPU box shares a large host: its cgroup/affinity share)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):  # pragma: no cover
+        return os.cpu_count() or 1

@@ -89,35 +89,13 @@ def render_frame_distributed(scene: Scene3D, render_service, *, group=None, row_
     """Every rank renders its interleaved row tile; one gather to ``dst``; ``dst`` returns the
     frame ([3, H*W] colour, or [H, W, 3] uint8 with ``gather="u8"``), the other ranks None.
 
-    ``render_service.render_tile(scene, row_block, n_parts, part, out)`` renders one tile
-    (``HipRenderer.render_tile``)."""
-    import torch
-    import torch.distributed as dist
+    ``render_service.render_tile(scene, row_block, n_parts, part, out[, into])`` renders one tile
+    (``HipRenderer.render_tile``). The buffers, the gather and the device un-permute live in
+    ``distributed.TileGather`` (cached per renderer and frame shape)."""
+    from python_ray_tracer_amd.distributed import tile_gather_for
 
-    from python_ray_tracer_amd.tiling import assemble, max_local_rows, n_local_rows
-
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    W, H = int(scene.camera.width), int(scene.camera.height)
     out = "u8" if gather == "u8" else None
-    tile = render_service.render_tile(scene, row_block, world, rank, out)
-    rows = n_local_rows(H, row_block, world, rank)
-    rmax = max_local_rows(H, row_block, world)
-    if rows < rmax:  # pad: the collective needs equal shapes
-        if out == "u8":
-            pad = torch.zeros((rmax - rows, W, 3), dtype=tile.dtype, device=tile.device)
-            tile = torch.cat([tile, pad], 0)
-        else:
-            pad = torch.zeros((tile.shape[0], (rmax - rows) * W), dtype=tile.dtype, device=tile.device)
-            tile = torch.cat([tile, pad], 1)
-    tile = tile.contiguous()
-    if dist.get_backend(group) == "gloo" and tile.is_cuda:  # gloo gathers host tensors
-        tile = tile.cpu()
-    gathered = [torch.empty_like(tile) for _ in range(world)] if rank == dst else None
-    dist.gather(tile, gathered, dst=dst, group=group)
-    if rank != dst:
-        return None
-    return assemble(gathered, H, W, row_block, layout="hwc" if out == "u8" else "soa")
+    return tile_gather_for(render_service, scene, group=group, row_block=row_block, dst=dst, out=out).render(scene)
 
 
 def render_frames(frames, render_service, output_dir=None, *, group=None, name: str = "frame_{:04d}.png",

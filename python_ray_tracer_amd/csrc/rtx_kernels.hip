@@ -1312,6 +1312,16 @@ template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>()>
 __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? (B >= 5 ? RTX_B5_WAVES : RTX_LV_WAVES) : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
+  {
+    // a blob that is not a packed scene of p.nsph spheres (the LDS table and every sphere loop are
+    // sized by p.nsph): render nothing and flag it (block-uniform, so the persistent launch's
+    // fetch counters stay untouched)
+    const cdouble* sc = (const cdouble*)p.scene;
+    if (sc[RTX_H_MAGIC] != RTX_MAGIC || sc[RTX_H_NSPH] != (double)p.nsph) {
+      if (threadIdx.x == 0) atomicOr((uint32_t*)p.ws + RTX_WS_STATUS, (uint32_t)RTX_ST_BAD_SCENE);
+      return;
+    }
+  }
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
                         // in fast_tile, after the first tile's level-0 nearest-hit test)
     const double* src = p.scene + RTX_HDR_WORDS;
@@ -1652,6 +1662,38 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const T* __restrict__ c, in
   out[3 * i + 2] = quant_u8((double)c[2 * n + i]);
 }
 
+// Rows of part p of the interleaved row tiling (python_ray_tracer_amd/tiling.py n_local_rows).
+__host__ __device__ __forceinline__ int tile_local_rows(int height, int row_block, int n_parts, int p) {
+  const int cycle = row_block * n_parts;
+  const int q = height / cycle, rem = height % cycle - p * row_block;
+  return q * row_block + (rem < 0 ? 0 : rem > row_block ? row_block : rem);
+}
+
+// Un-permute of gathered row tiles (the multi-GPU frame, application.render_frame_distributed):
+// part p's buffer (at tiles + p * part_stride) holds its rows in local order, as rtx_render_camera
+// wrote them, [planes][rows_p][row_bytes]; the frame is [planes][height][row_bytes]. One block per
+// (frame row, plane): a contiguous row copy, 16 B per lane when the row and buffers allow it.
+__global__ __launch_bounds__(kBlock) void k_assemble_rows(const uint8_t* __restrict__ tiles, int64_t part_stride,
+                                                          int n_parts, int height, int row_block, int64_t row_bytes,
+                                                          bool vec16, uint8_t* __restrict__ out) {
+  const int g = blockIdx.x;  // frame row
+  const int c = blockIdx.y;  // plane
+  const int b = g / row_block;
+  const int p = b % n_parts;
+  const int lr = (b / n_parts) * row_block + g % row_block;
+  const int rows_p = tile_local_rows(height, row_block, n_parts, p);
+  const uint8_t* src = tiles + p * part_stride + ((int64_t)c * rows_p + lr) * row_bytes;
+  uint8_t* dst = out + ((int64_t)c * height + g) * row_bytes;
+  if (vec16) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* s4 = (const u32x4*)src;
+    u32x4* d4 = (u32x4*)dst;
+    for (int64_t k = threadIdx.x; k < row_bytes / 16; k += kBlock) __builtin_nontemporal_store(s4[k], d4 + k);
+  } else {
+    for (int64_t k = threadIdx.x; k < row_bytes; k += kBlock) dst[k] = src[k];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -1675,6 +1717,8 @@ int check_launch(const char* what) {
 // Optional live timing of the dominant kernel (bench.py's roofline): a pool of event pairs handed to
 // the k_render_fast launch itself (hipExtLaunchKernelGGL), so they time the dispatch from its start
 // to its end, as rocprofv3's kernel trace does, without the gap an event recorded before it adds.
+// The state belongs to the calling thread: render calls from other threads are never timed by it
+// and never touch it (the entry points stay re-entrant).
 struct Prof {
   int cap = 0;
   int used = 0;
@@ -1682,7 +1726,8 @@ struct Prof {
   int every = 1;             // record one launch in `every` (rtx_profile_sample)
   long long seen = 0;        // launches since rtx_profile_enable
   bool on = false;           // the current launch is recorded
-} g_prof;
+};
+thread_local Prof g_prof;
 
 void prof_free() {
   for (int i = 0; i < 2 * g_prof.cap; ++i) (void)hipEventDestroy(g_prof.ev[i]);
@@ -2128,6 +2173,33 @@ int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, 
     return fail(RTX_E_ARG, "bad color_kind%s %lld", "", color_kind);
   }
   return check_launch("k_quantize");
+}
+
+int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts, int width, int height,
+                      int row_block, int kind, void* out, void* stream) {
+  if (!tiles || !out) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0) return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  int planes = 3;
+  int64_t row_bytes;
+  if (kind == RTX_OUT_F32_SOA) {
+    row_bytes = 4 * (int64_t)width;
+  } else if (kind == RTX_OUT_F64_SOA) {
+    row_bytes = 8 * (int64_t)width;
+  } else if (kind == RTX_OUT_U8_HWC) {
+    row_bytes = 3 * (int64_t)width;
+    planes = 1;
+  } else {
+    return fail(RTX_E_ARG, "bad kind%s %lld", "", kind);
+  }
+  const int rmax = tile_local_rows(height, row_block, n_parts, 0);  // part 0 has the most rows
+  if (part_stride_bytes < planes * rmax * row_bytes)
+    return fail(RTX_E_ARG, "part_stride too small%s (need %lld bytes)", "", (long long)(planes * rmax * row_bytes));
+  const bool vec16 = row_bytes % 16 == 0 && part_stride_bytes % 16 == 0 && (uintptr_t)tiles % 16 == 0 &&
+                     (uintptr_t)out % 16 == 0;
+  hipLaunchKernelGGL(k_assemble_rows, dim3((unsigned)height, (unsigned)planes), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const uint8_t*)tiles, part_stride_bytes, n_parts, height, row_block, row_bytes, vec16,
+                     (uint8_t*)out);
+  return check_launch("k_assemble_rows");
 }
 
 }  // extern "C"

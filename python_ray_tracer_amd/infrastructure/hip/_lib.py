@@ -36,6 +36,7 @@ OUT_U8_HWC = 2
 
 ST_STACK_OVERFLOW = 1
 ST_LIST_OVERFLOW = 2
+ST_BAD_SCENE = 4
 
 # header words
 H_MAGIC, H_NSPH, H_CAM, H_LIGHT, H_DOMEC, H_NDOME, H_DOMEI = 0, 1, 2, 5, 8, 11, 12
@@ -68,6 +69,7 @@ EXPORTS = (
     "rtx_profile_collect",
     "rtx_profile_sample",
     "rtx_selftest_math",
+    "rtx_assemble_rows",
 )
 
 _c_void_p = ctypes.c_void_p
@@ -92,6 +94,7 @@ _SIGS = {
     "rtx_profile_collect": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
     "rtx_profile_sample": (_i32, [_i32]),
     "rtx_selftest_math": (_i32, [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "rtx_assemble_rows": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
 }
 
 _lib = None

@@ -24,6 +24,7 @@ Differences from the reference, all deliberate and documented in DESIGN.md:
 from __future__ import annotations
 
 import numbers
+import os
 from pathlib import Path
 
 import numpy as np
@@ -241,6 +242,8 @@ class HipRenderer(Renderer):
             status = int(ws[:8].view(torch.int32)[1].item())
             if status:
                 ws[4:8].zero_()  # sticky flags: clear for the next call
+            if status & L.ST_BAD_SCENE:
+                raise ValueError("the scene blob's header disagrees with n_spheres: nothing was rendered")
             if status & L.ST_STACK_OVERFLOW:
                 raise RecursionError(f"maximum recursion depth exceeded (reflection chain > {L.UNBOUNDED_LEVELS} levels)")
 
@@ -270,24 +273,37 @@ class HipRenderer(Renderer):
         return HipRGBColor.from_tensor(self.render_tile(scene))
 
     def render_tile(self, scene, row_block: int = 1, n_parts: int = 1, part: int = 0, out: str | None = None,
-                    blob: torch.Tensor | None = None, n_spheres: int | None = None) -> torch.Tensor:
+                    blob: torch.Tensor | None = None, n_spheres: int | None = None,
+                    into: torch.Tensor | None = None) -> torch.Tensor:
         """Render the interleaved row tile ``part`` of ``n_parts`` (row blocks of ``row_block``) of
         the scene camera's frame. Returns [3, rows*W] colour (``out=None``) or [rows, W, 3] uint8
-        (``out="u8"``), rows in local order (python_ray_tracer_amd.tiling.tile_rows)."""
+        (``out="u8"``), rows in local order (python_ray_tracer_amd.tiling.tile_rows).
+
+        ``into``: a contiguous device tensor of that shape and dtype to render into (a
+        pre-allocated gather buffer) instead of a new one. ``blob``/``n_spheres``: an already
+        packed device scene (checked against its header)."""
         from python_ray_tracer_amd.tiling import n_local_rows
 
         cam = scene.camera
         W, H = int(cam.width), int(cam.height)
         if blob is None:
             blob, n_spheres = self.scene_blob(scene)
+        else:
+            _check_blob(blob, n_spheres, self.device)
         rows = n_local_rows(H, row_block, n_parts, part)
         n = W * rows
         if out == "u8":
-            res = torch.empty((rows, W, 3), dtype=torch.uint8, device=self.device)
-            kind = L.OUT_U8_HWC
+            shape, dtype, kind = (rows, W, 3), torch.uint8, L.OUT_U8_HWC
         else:
-            res = torch.empty((3, n), dtype=self.color_dtype, device=self.device)
-            kind = _OUT_KIND[self.color_dtype]
+            shape, dtype, kind = (3, n), self.color_dtype, _OUT_KIND[self.color_dtype]
+        if into is None:
+            res = torch.empty(shape, dtype=dtype, device=self.device)
+        else:
+            if (tuple(into.shape) != shape or into.dtype != dtype or into.device != self.device
+                    or not into.is_contiguous()):
+                raise ValueError(f"into: need a contiguous {dtype} tensor of shape {shape} on {self.device}, got "
+                                 f"{into.dtype} {tuple(into.shape)} on {into.device}")
+            res = into
         ws = self.workspace(n)
         L.check(self._lib.rtx_render_camera(blob.data_ptr(), n_spheres, W, H, row_block, n_parts, part, rows,
                                             self._bounces_arg, res.data_ptr(), kind, ws.data_ptr(), ws.numel(),
@@ -382,7 +398,9 @@ class HipRenderer(Renderer):
             t = t.reshape(3, 1)
         if t.dtype not in _OUT_KIND:
             t = t.to(torch.float64)
-        t = t.contiguous()
+        # a colour assembled on the host (a gloo gather) or built by the caller from CPU tensors:
+        # the kernel reads device memory only
+        t = t.to(self.device).contiguous()
         n = t.shape[1]
         if n != W * H:
             # np.reshape in save_image (base.py:147)
@@ -391,6 +409,24 @@ class HipRenderer(Renderer):
         L.check(self._lib.rtx_quantize_u8(t.data_ptr(), _OUT_KIND[t.dtype], n, out.data_ptr(), self._stream()),
                 "rtx_quantize_u8")
         return out
+
+    def assemble_rows(self, tiles: torch.Tensor, width: int, height: int, row_block: int,
+                      out: str | None = None) -> torch.Tensor:
+        """Frame from gathered row tiles (rtx_assemble_rows, the device un-permute of the
+        multi-GPU path): ``tiles`` is [n_parts, part_len], part p holding render_tile(...,
+        row_block, n_parts, p, out) flattened at its start. Returns what a whole-frame
+        render_tile returns: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``)."""
+        P = int(tiles.shape[0])
+        tiles = tiles.to(self.device).contiguous()
+        if out == "u8":
+            kind, res = L.OUT_U8_HWC, torch.empty((height, width, 3), dtype=torch.uint8, device=self.device)
+        else:
+            kind = _OUT_KIND[tiles.dtype]
+            res = torch.empty((3, height * width), dtype=tiles.dtype, device=self.device)
+        stride = tiles.stride(0) * tiles.element_size()
+        L.check(self._lib.rtx_assemble_rows(tiles.data_ptr(), stride, P, width, height, row_block, kind,
+                                            res.data_ptr(), self._stream()), "rtx_assemble_rows")
+        return res
 
     def stats(self) -> dict:
         """Per-level counters accumulated since construction / reset_stats (synchronises)."""
@@ -419,6 +455,26 @@ def _as_vector(v) -> HipVector3D:
     raise TypeError(f"expected a 3-vector, got {type(v).__name__}")
 
 
+def _check_blob(blob: torch.Tensor, n_spheres, device) -> None:
+    """A caller-supplied packed scene: float64, contiguous, on the renderer's device, and its
+    header's sphere count equal to ``n_spheres`` (the kernels size the LDS table and every sphere
+    loop by it). Reads the header back: one small synchronous copy."""
+    if not isinstance(blob, torch.Tensor) or blob.dtype != torch.float64 or blob.dim() != 1 or not blob.is_contiguous():
+        raise ValueError("blob: need a contiguous 1-D float64 tensor (scene_pack.pack_scene)")
+    if blob.device != torch.device(device):
+        raise ValueError(f"blob is on {blob.device}, the renderer on {device}")
+    if blob.numel() < L.HDR_WORDS:
+        raise ValueError("blob shorter than the scene header")
+    hdr = blob[:L.H_NSPH + 1].cpu().tolist()
+    if hdr[L.H_MAGIC] != L.MAGIC:
+        raise ValueError("blob is not a packed scene (bad magic)")
+    if n_spheres is None or int(hdr[L.H_NSPH]) != int(n_spheres):
+        raise ValueError(f"n_spheres={n_spheres!r} but the blob holds {int(hdr[L.H_NSPH])} spheres")
+    need = L.HDR_WORDS + int(hdr[L.H_NSPH]) * (L.GEOM_WORDS + L.MAT_WORDS)
+    if blob.numel() < need:
+        raise ValueError(f"blob too short for {int(hdr[L.H_NSPH])} spheres ({blob.numel()} < {need} words)")
+
+
 def _same_point(a, b) -> bool:
     try:
         return all(np.ndim(u) == 0 and float(u) == float(w) for u, w in zip(_as_vector(a).components(),
@@ -439,5 +495,10 @@ def _write_png(hwc: np.ndarray, output_path) -> None:
     img = Image.fromarray(np.ascontiguousarray(hwc, dtype=np.uint8))
     if hasattr(output_path, "write"):  # file object: PNG (a path's extension picks the format, like PIL in base.py:151)
         img.save(output_path, format="PNG")
-    else:
-        img.save(Path(output_path))
+        return
+    # written to a temporary name and renamed, so an interrupted write never leaves a truncated
+    # file under the final name (render_frames treats an existing file as finished)
+    path = Path(output_path)
+    tmp = path.with_name(path.name + ".tmp")
+    img.save(tmp, format=Image.registered_extensions().get(path.suffix.lower(), "PNG"))
+    os.replace(tmp, path)

@@ -5,6 +5,12 @@ balances the load: sky rows (no hit, ~15 flops/pixel) and ground rows (thousands
 across ranks instead of landing on one rank as contiguous strips would. Local row ``lr`` of part
 ``p`` is global row ``((lr // rb) * P + p) * rb + lr % rb`` — the mapping the kernel uses
 (``global_row`` in rtx_kernels.hip).
+
+Gather layout: every part travels as one flat buffer of ``part_len`` elements (the same length on
+every rank, as a collective needs), holding that part's tile exactly as ``render_tile`` returns
+it — colour ``[3, rows_p*W]`` or uint8 ``[rows_p, W, 3]`` — at its start. ``assemble`` is the
+host-side un-permute of such buffers (CPU tensors / NumPy); on the GPU the same layout is
+un-permuted by ``rtx_assemble_rows``.
 """
 
 from __future__ import annotations
@@ -28,38 +34,43 @@ def tile_rows(height: int, row_block: int, n_parts: int, part: int) -> np.ndarra
 
 
 def max_local_rows(height: int, row_block: int, n_parts: int) -> int:
-    return max(n_local_rows(height, row_block, n_parts, p) for p in range(n_parts))
+    return n_local_rows(height, row_block, n_parts, 0)  # part 0 has the most rows
 
 
-def assemble(tiles, height: int, width: int, row_block: int, layout: str = "soa"):
-    """Un-permute gathered tiles into one frame.
+def tile_shape(height: int, width: int, row_block: int, n_parts: int, part: int, out: str | None = None):
+    """Shape ``render_tile`` returns for this part: (3, rows*W) colour or (rows, W, 3) uint8."""
+    rows = n_local_rows(height, row_block, n_parts, part)
+    return (rows, int(width), 3) if out == "u8" else (3, rows * int(width))
 
-    ``tiles[p]`` is part p's tile padded to the same row count: ``[C, rows_max*W]`` (layout "soa",
-    colour planes) or ``[rows_max, W, 3]`` (layout "hwc", uint8 pixels). Works on torch tensors
-    (device-side index copy) and on NumPy arrays."""
+
+def part_len(height: int, width: int, row_block: int, n_parts: int, itemsize: int, out: str | None = None) -> int:
+    """Elements of one gather buffer: the largest part's tile, rounded up to 16 bytes (so every
+    part of a [n_parts, part_len] buffer starts 16-byte aligned for the device copy)."""
+    n = 3 * max_local_rows(height, row_block, n_parts) * int(width)
+    per16 = max(1, 16 // itemsize)
+    return (n + per16 - 1) // per16 * per16
+
+
+def assemble(tiles, height: int, width: int, row_block: int, out: str | None = None):
+    """Un-permute gathered part buffers ``tiles[p]`` (each ``part_len`` long, layout above) into
+    one frame: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``). Torch tensors or NumPy arrays."""
     import torch
 
     n_parts = len(tiles)
     first = tiles[0]
     is_torch = isinstance(first, torch.Tensor)
-    if layout == "soa":
-        C = first.shape[0]
-        full = (torch.empty((C, height, width), dtype=first.dtype, device=first.device) if is_torch
-                else np.empty((C, height, width), dtype=first.dtype))
-    else:
-        full = (torch.empty((height, width, 3), dtype=first.dtype, device=first.device) if is_torch
-                else np.empty((height, width, 3), dtype=first.dtype))
-    for p, t in enumerate(tiles):
+    shape = (height, width, 3) if out == "u8" else (3, height, width)
+    full = (torch.empty(shape, dtype=first.dtype, device=first.device) if is_torch
+            else np.empty(shape, dtype=first.dtype))
+    for p in range(n_parts):
         rows = tile_rows(height, row_block, n_parts, p)
         k = len(rows)
         if k == 0:
             continue
         idx = torch.as_tensor(rows, device=first.device) if is_torch else rows
-        if layout == "soa":
-            src = t.reshape(t.shape[0], -1, width)[:, :k]
-            full[:, idx] = src
+        src = tiles[p][:3 * k * width]
+        if out == "u8":
+            full[idx] = src.reshape(k, width, 3)
         else:
-            full[idx] = t[:k]
-    if layout == "soa":
-        return full.reshape(full.shape[0], height * width)
-    return full
+            full[:, idx] = src.reshape(3, k, width)
+    return full if out == "u8" else full.reshape(3, height * width)

@@ -1,0 +1,41 @@
+"""The multi-rank render path with HipRenderer tiles on the GPU.
+
+The box has one GPU and RCCL needs one GPU per rank, so two fresh torchrun ranks share the GPU
+over gloo (tiles travel through host memory; on an 8-GPU node the same code runs over RCCL). The
+frame they gather and assemble on the device must equal the single-rank frame bit for bit — colour
+and uint8 gathers, capped and unbounded bounces, a 65-sphere scene — and render_image_pipeline's
+PNG must equal the single-rank pipeline's. Also the two-slot pipelined gather (bench --mode tiles).
+"""
+
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_ranks_share_gpu_gather_equals_single_frame(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(REPO / "tests" / "dist_hip_worker.py"),
+           str(tmp_path)]
+    p = subprocess.run(cmd, cwd=str(REPO), env=env, capture_output=True, text=True, timeout=110)
+    logs = {f.name: f.read_text() for f in tmp_path.glob("rank*.txt")}
+    assert p.returncode == 0, (p.returncode, logs, p.stdout[-3000:], p.stderr[-3000:])
+    assert set(logs) == {"rank0.txt", "rank1.txt"}, logs
+    assert "False" not in logs["rank0.txt"] and "png_u8" in logs["rank0.txt"], logs

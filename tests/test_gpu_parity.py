@@ -117,16 +117,31 @@ def test_row_tiles_reassemble(hip):
 
     spec = scenes.readme_spec(200, 117)
     scene = scenes.build_scene(spec)
-    r = hip.HipRenderer(max_bounces=3)
-    full = r.render(scene).data
-    for P, rb in ((2, 8), (3, 5), (8, 8)):
-        tiles = [r.render_tile(scene, rb, P, p) for p in range(P)]
-        rmax = tiling.max_local_rows(117, rb, P)
-        padded = [torch.nn.functional.pad(t, (0, rmax * 200 - t.shape[1])) for t in tiles]
-        assert torch.equal(tiling.assemble(padded, 117, 200, rb), full)
-        u8 = [r.render_tile(scene, rb, P, p, out="u8") for p in range(P)]
-        u8 = [torch.nn.functional.pad(t, (0, 0, 0, 0, 0, rmax - t.shape[0])) for t in u8]
-        assert torch.equal(tiling.assemble(u8, 117, 200, rb, layout="hwc"), r.quantize(r.render(scene), scene.camera))
+    full_u8 = None
+    for dtype in (torch.float64, torch.float32):
+        r = hip.HipRenderer(max_bounces=3, color_dtype=dtype)
+        full = r.render(scene).data
+        full_u8 = r.quantize(r.render(scene), scene.camera)
+        for P, rb in ((2, 8), (3, 5), (8, 8), (5, 1)):
+            for out, ref, isz in ((None, full, full.element_size()), ("u8", full_u8, 1)):
+                n = tiling.part_len(117, 200, rb, P, isz, out)
+                # tiles rendered straight into the gather buffers (render_tile(into=)), then the
+                # device un-permute (rtx_assemble_rows) and the host one (tiling.assemble)
+                buf = torch.full((P, n), 7, dtype=ref.dtype, device=ref.device)
+                for p in range(P):
+                    shp = tiling.tile_shape(117, 200, rb, P, p, out)
+                    view = buf[p, :int(np.prod(shp))].view(shp)
+                    r.render_tile(scene, rb, P, p, out=out, into=view)
+                    assert torch.equal(view, r.render_tile(scene, rb, P, p, out=out))
+                assert torch.equal(r.assemble_rows(buf, 200, 117, rb, out), ref), (P, rb, out)
+                assert torch.equal(tiling.assemble(buf.cpu(), 117, 200, rb, out), ref.cpu()), (P, rb, out)
+                assert torch.equal(r.assemble_rows(buf.cpu(), 200, 117, rb, out), ref)  # host tiles
+    with pytest.raises(ValueError):
+        r.render_tile(scene, 8, 2, 0, into=torch.empty(5, device="cuda"))
+    blob, S = r.scene_blob(scene)
+    with pytest.raises(ValueError):
+        r.render_tile(scene, blob=blob, n_spheres=S + 1)
+    assert torch.equal(r.render_tile(scene, blob=blob, n_spheres=S), full)
 
 
 def test_render_batch_matches_single_frames(hip):

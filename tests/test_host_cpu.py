@@ -171,18 +171,24 @@ def test_tiling_partition(H, rb, P):
         r = tiling.tile_rows(H, rb, P, p)
         assert len(r) == tiling.n_local_rows(H, rb, P, p)
         assert np.all(np.diff(r) > 0)
-    # assemble inverts the split
+    assert tiling.max_local_rows(H, rb, P) == max(tiling.n_local_rows(H, rb, P, p) for p in range(P))
+    # assemble inverts the split, from the flat gather buffers (colour and uint8 layouts)
     W = 3
     frame = np.arange(3 * H * W, dtype=np.float64).reshape(3, H, W)
-    rmax = tiling.max_local_rows(H, rb, P)
-    tiles = []
+    L = tiling.part_len(H, W, rb, P, 8)
+    assert L >= 3 * tiling.max_local_rows(H, rb, P) * W and (L * 8) % 16 == 0
+    tiles = np.full((P, L), -1.0)
+    hwc = (frame.reshape(3, H * W).T.reshape(H, W, 3) % 251).astype(np.uint8)
+    L8 = tiling.part_len(H, W, rb, P, 1, "u8")
+    tiles8 = np.zeros((P, L8), dtype=np.uint8)
     for p in range(P):
         r = tiling.tile_rows(H, rb, P, p)
-        t = np.zeros((3, rmax, W))
-        t[:, :len(r)] = frame[:, r]
-        tiles.append(torch.from_numpy(t.reshape(3, rmax * W)))
-    full = tiling.assemble(tiles, H, W, rb).numpy()
-    assert np.array_equal(full, frame.reshape(3, H * W))
+        assert tiling.tile_shape(H, W, rb, P, p) == (3, len(r) * W)
+        tiles[p, :3 * len(r) * W] = frame[:, r].reshape(-1)
+        tiles8[p, :3 * len(r) * W] = hwc[r].reshape(-1)
+    assert np.array_equal(tiling.assemble(tiles, H, W, rb), frame.reshape(3, H * W))
+    assert np.array_equal(tiling.assemble(torch.from_numpy(tiles), H, W, rb).numpy(), frame.reshape(3, H * W))
+    assert np.array_equal(tiling.assemble(tiles8, H, W, rb, "u8"), hwc)
 
 
 def test_hip_renderer_fails_loudly_without_gpu():
