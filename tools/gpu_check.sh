@@ -40,4 +40,4 @@ if [ "${GC_PROF:-0}" = 1 ]; then
 fi
 cat "$OUT/status.txt"
 grep -E "passed|failed|error" "$OUT/pytest_gpu.log" | tail -3
-cat "$OUT/bench.json" "$OUT/bench_2rank.json" 2>/dev/null
+cat "$OUT/bench.json" "$OUT/bench_2rank.json" 2>/dev/null || true
