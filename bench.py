@@ -50,8 +50,10 @@ def parse():
                          "the uint8 image save_image writes)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N>1: skip the extra weak-scaling frames and C4-tiles measurements")
-    ap.add_argument("--cpu-procs", type=int, default=16,
-                    help="processes of the row-tiled all-cores CPU baseline (the box's CPU share is 16)")
+    ap.add_argument("--cpu-procs", type=int, default=14,
+                    help="processes of the row-tiled all-cores CPU baseline (the box's CPU share is 16 cores, and "
+                         "at most 16 processes may hold the GPU open: importing torch opens it in every worker, "
+                         "so 14 workers + this process)")
     ap.add_argument("--frames-per-step", type=int, default=1,
                     help="frames mode: render this many orbit frames of the config (C5 camera path, "
                          "SURVEY.md 8d) per step in ONE launch (rtx_render_frames)")
