@@ -154,6 +154,8 @@ enum {
   RTX_S_PIXELS = 0,   /* rays started at level 0               */
   RTX_S_DEFERRED = 1, /* rays handed to the general (tie/deep) kernel */
   RTX_S_TIES = 2,     /* (ray, level) pairs with >1 nearest shape */
+  RTX_S_TESTS = 3,    /* ray-sphere tests executed by live lanes (fast kernel; culling skips most) */
+  RTX_S_NODES = 4,    /* culling-node (box) tests executed by live lanes (fast kernel)            */
   RTX_S_LEVELS = 64,  /* levels recorded                        */
   RTX_S_RAYS = 8,     /* [8 .. 8+64): rays traced per level     */
   RTX_S_HITS = 72,    /* [72 .. 72+64): shaded hits (= shadow rays) per level */

@@ -23,7 +23,7 @@
 //                     a tree of boxes that the loops walk wave-uniformly (exact culling). Tile rows
 //                     are dispatched bottom-up (longest work first). A ray that meets a tie (two
 //                     shapes at the same nearest distance, base.py:103 — both get shaded and summed)
-//                     or, under a cap above 8 or none, a chain longer than RTX_DEEP_LEVELS levels is
+//                     or, under a cap above 8 or none, a chain longer than kDeepLevels levels is
 //                     appended to a deferred list.
 //   k_render_general  Any bounce cap, ties included: an explicit depth-first walk of the ray tree
 //                     with per-worker frame stacks in the workspace (HBM). Renders the deferred
@@ -46,88 +46,60 @@
 namespace {
 
 constexpr int kBlock = 256;   // threads per block of the elementwise boundary kernels
-#ifndef RTX_WAVE_W
-#define RTX_WAVE_W 8  // pixels per wave row: a wave renders an RTX_WAVE_W x (64 / RTX_WAVE_W) tile
-#endif
-constexpr int kWaveW = RTX_WAVE_W;
+// ---- tuning constants (each value chosen by an A/B on identical output, profiles/r1_ab_variants.txt;
+// tools/ab_build.py builds variants by rewriting these lines) ----
+constexpr int kWaveW = 8;       // pixels per wave row: a wave renders a kWaveW x (64 / kWaveW) tile
+constexpr int kFastWaves = 4;   // waves per k_render_fast block (1, 2 or 4)
+// k_render_fast single-frame launches of scenes with at least this many spheres: persistent waves
+// fetching wave tiles (A/B: 65 spheres -14%, 17 spheres +-0, 3-16 spheres without the culling tree
+// +12%: their tiles are short, so the ramp-up of the fetch counters and the drain cost more than
+// the balancing gains)
+constexpr int kPersistMinSpheres = 32;
+constexpr int kMaxFetch = 32;   // tile counters (one 128-byte line each) shared round-robin by the waves
+// general-kernel threads: ties only (caps <= RTX_FAST_MAX_BOUNCES; an empty launch costs more with
+// more blocks), or ties and deep chains (A/B for unbounded renders: 4096, 16384, 65536)
+constexpr int kDeferredWorkers = 4096;
+constexpr int kDeepWorkers = 16384;
+constexpr bool kLevelsInLds = true;  // capped kernels with B <= kLevelsLdsMaxB keep their levels' colour inputs in LDS
+constexpr int kLevelsLdsMaxB = 6;    // the deepest cap with LDS level slots
+constexpr int kLevelsLdsSlots = 3;   // levels kept in LDS; deeper ones (B = 4) in a register slot
+constexpr int kB5Slots = 2;          // LDS level slots of the B >= 5 kernels (the others in a register shift)
+constexpr int kB5Waves = 4;          // their waves/SIMD
+constexpr int kLvWaves = 5;          // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
+constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
+constexpr int kDeepWaves = 3;        // waves/SIMD of the DEEP instantiation (records + continuation need registers)
+constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
+constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
+                                     // 8-level instantiation spills, 3 defers too many pixels)
+constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k_render_fast<cap>
+// ---- derived ----
 constexpr int kWaveH = 64 / kWaveW;
-#ifndef RTX_BLOCK_WAVES
-#define RTX_BLOCK_WAVES 4  // waves per k_render_fast block (1, 2 or 4)
-#endif
-constexpr int kFastWaves = RTX_BLOCK_WAVES;
-static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "RTX_BLOCK_WAVES");
+static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
+static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "kMaxFetch must be a power of two");
 constexpr int kFastBlock = 64 * kFastWaves;
 constexpr int kWavesX = kFastWaves == 1 ? 1 : 2;  // block tile: kWavesX x kWavesY waves
 constexpr int kWavesY = kFastWaves / kWavesX;
 constexpr int kTileW = kWavesX * kWaveW;
 constexpr int kTileH = kWavesY * kWaveH;
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
-// k_render_fast single-frame launches of scenes with at least this many spheres: persistent waves
-// fetching wave tiles (A/B: 65 spheres -14%, 17 spheres +-0, 3-16 spheres without the culling tree
-// +12%: their tiles are short, so the ramp-up of the fetch counters and the drain cost more than
-// the balancing gains)
-#ifndef RTX_PERSIST_MIN_SPHERES
-#define RTX_PERSIST_MIN_SPHERES 32
-#endif
-#ifndef RTX_FETCH_COUNTERS
-#define RTX_FETCH_COUNTERS 32  // tile counters (one 128-byte line each) shared round-robin by the waves
-#endif
-constexpr int kMaxFetch = RTX_FETCH_COUNTERS;
 constexpr int kFetchStride = 32;  // uint32 words between counters
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
 constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this size (32 KiB)
-// general-kernel threads: ties only (caps <= RTX_FAST_MAX_BOUNCES; an empty launch costs more with
-// more blocks), or ties and deep chains (A/B for unbounded renders: 4096, 16384, 65536)
-#ifndef RTX_DEFERRED_WORKERS
-#define RTX_DEFERRED_WORKERS 4096
-#endif
-#ifndef RTX_DEEP_WORKERS
-#define RTX_DEEP_WORKERS 16384
-#endif
-constexpr int kDeferredWorkers = RTX_DEFERRED_WORKERS;
-#ifndef RTX_LEVELS_IN_LDS
-#define RTX_LEVELS_IN_LDS 1  // capped kernels with B <= RTX_LEVELS_LDS_MAXB keep their levels' colour inputs in LDS
-#endif
-#ifndef RTX_LEVELS_LDS_MAXB
-#define RTX_LEVELS_LDS_MAXB 6  // the deepest cap with LDS level slots
-#endif
-#ifndef RTX_B5_SLOTS
-#define RTX_B5_SLOTS 2  // LDS level slots of the B = 5 kernel (the others in a register shift)
-#endif
-#ifndef RTX_B5_WAVES
-#define RTX_B5_WAVES 4  // its waves/SIMD
-#endif
-#ifndef RTX_LEVELS_LDS_SLOTS
-#define RTX_LEVELS_LDS_SLOTS 3  // levels kept in LDS; deeper ones (B = 4) in a register slot
-#endif
-#ifndef RTX_LV_WAVES
-#define RTX_LV_WAVES 5  // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
-#endif
 // The colour inputs of the non-terminal levels (4 doubles + the key per level and lane) go to LDS
 // slots indexed by the level instead of a register shift register (no moves per level, 27 fewer
 // live VGPRs): [B][4][kFastBlock] doubles + [B][kFastBlock] ints after the scene table.
 template <int B, bool LDS, bool DEEP>
-constexpr bool levels_in_lds() { return RTX_LEVELS_IN_LDS && LDS && !DEEP && B > 0 && B <= RTX_LEVELS_LDS_MAXB; }
+constexpr bool levels_in_lds() { return kLevelsInLds && LDS && !DEEP && B > 0 && B <= kLevelsLdsMaxB; }
 // the DEEP variant (3 waves/SIMD: 3 blocks per CU) keeps all its levels in LDS
 template <bool DEEP = false>
 __host__ __device__ constexpr int level_lds_slots(int B) {
-  return DEEP || B < RTX_LEVELS_LDS_SLOTS ? B : B >= 5 ? RTX_B5_SLOTS : RTX_LEVELS_LDS_SLOTS;
+  return DEEP || B < kLevelsLdsSlots ? B : B >= 5 ? kB5Slots : kLevelsLdsSlots;
 }
 template <bool DEEP = false>
 __host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)level_lds_slots<DEEP>(B) * kFastBlock * (4 * 8 + 4); }
-#ifndef RTX_DEEP_LV_MAX_SPHERES
-#define RTX_DEEP_LV_MAX_SPHERES 32  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
-#endif
-constexpr int kDeepWorkers = RTX_DEEP_WORKERS;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
-#ifndef RTX_DEEP_WAVES
-#define RTX_DEEP_WAVES 3  // the same for the DEEP instantiation (records + continuation need registers)
-#endif
-#ifndef RTX_FAST_WAVES
-#define RTX_FAST_WAVES 4  // __launch_bounds__ min waves per SIMD for k_render_fast: <=128 VGPRs (A/B: faster than 3 waves without spills)
-#endif
 
 // Wave-uniform loads through the scalar cache: the constant address space makes hipcc emit s_load
 // even though the kernel also stores (it cannot prove the scene blob is not aliased otherwise).
@@ -168,7 +140,7 @@ struct Params {
   int64_t n_workers;
   int stack_levels;
   unsigned long long* stats;
-  int n_tiles_x, n_tiles_y;  // persistent launch of k_render_fast (0: one tile per block)
+  int n_tiles_x, n_tiles_y;  // persistent launch of k_render_fast (wave tiles; 0: one block tile per block)
   // persistent waves (n_fetch > 0): wave tiles (kWaveW x kWaveH) handed out by n_fetch counters
   uint32_t* fetch;
   int n_fetch;
@@ -186,19 +158,15 @@ constexpr int kFrameShift = 34;
 constexpr int kRaysShift = 50;
 constexpr int kHitsShift = 57;
 constexpr int kLevelMask = 0x7F;  // 7-bit level fields (level + 1)
-// Resume record of a pixel deferred for depth at level L = RTX_DEEP_LEVELS: the next level's ray
+// Resume record of a pixel deferred for depth at level L = kDeepLevels: the next level's ray
 // (origin, direction) and the colour inputs (dli, di, spec, va, key) of levels 0..L; the general
 // kernel continues the chain at level L + 1 instead of re-rendering it from level 0.
-#ifndef RTX_DEEP_LEVELS
-#define RTX_DEEP_LEVELS 5  // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
-                           // 8-level instantiation spills, 3 defers too many pixels)
-#endif
 constexpr int kRecLevelWords = 5;
 __host__ __device__ constexpr int rec_words(int level) { return 6 + kRecLevelWords * (level + 1); }
-constexpr int kDeepLevel2 = 2 * RTX_DEEP_LEVELS + 1;  // deferral level of the first continuation pass
-constexpr int kDeepLevel3 = 3 * RTX_DEEP_LEVELS + 2;  // ... and of the second
+constexpr int kDeepLevel2 = 2 * kDeepLevels + 1;  // deferral level of the first continuation pass
+constexpr int kDeepLevel3 = 3 * kDeepLevels + 2;  // ... and of the second
 static_assert(kDeepLevel3 + 2 < kLevelMask, "deferred-entry level fields hold 7 bits");
-// Resume-record capacities per deferral level (pass 0: the first pass's level RTX_DEEP_LEVELS;
+// Resume-record capacities per deferral level (pass 0: the first pass's level kDeepLevels;
 // 1, 2: the continuation passes'): at least 2^18 / 2^16 / 2^14, or one per 32 / 256 / 2048 pixels,
 // whichever is more. Chains alive at level 5 are 0.2-1.4% of the pixels in the bench scenes (C4:
 // 467,657 of 33.2 M), far fewer at 11 and 17. An entry beyond the capacity is re-rendered from
@@ -354,11 +322,7 @@ __device__ __forceinline__ int trunc_parity(double x) {
 // Below 1e-150, b*b may round up by far more than an ulp in the subnormal range (b = 1.6e-162, c = 0:
 // the reference reports a hit at 3.1e-163, tests/golden/intersect_kat.json), so those take the root.
 __device__ __forceinline__ bool behind(double b, double c) {
-#ifdef RTX_NO_BEHIND
-  return false;
-#else
   return b >= 1e-150 && c >= 0.0 && b <= 1e150;
-#endif
 }
 
 // NumpySphere.intersect, shape.py:28-51, for a ray with precomputed oo = O.O.
@@ -445,6 +409,21 @@ __device__ __forceinline__ void nearest_update(bool valid, double t, int s, doub
   }
 }
 
+// Executed-work counters of the stats launch (bench.py's executed-FLOP model): ray-sphere tests
+// and culling-node tests performed by each live lane. Work<false> (the timed kernels) compiles to
+// nothing.
+template <bool ON>
+struct Work {
+  __device__ __forceinline__ void test(int) {}
+  __device__ __forceinline__ void node() {}
+};
+template <>
+struct Work<true> {
+  uint32_t tests = 0, nodes = 0;
+  __device__ __forceinline__ void test(int k) { tests += (uint32_t)k; }
+  __device__ __forceinline__ void node() { ++nodes; }
+};
+
 // Shadow any-hit: does test j (root t, validity v) come strictly before the shape's own distance
 // t_self? An invalid test is FARAWAY, which is before t_self only when t_self > FARAWAY (far_self).
 __device__ __forceinline__ bool shadows(bool valid, double t, double tself, bool far_self) {
@@ -490,10 +469,11 @@ __device__ __forceinline__ bool node_may_hit(const cdouble* nd, double ox, doubl
 }
 
 // Nearest hit over entries [first, first + cnt) of the culled geometry list (pairs, scalar loads).
-template <bool CAM>
+template <bool CAM, typename Wk>
 __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int cnt, double ox, double oy, double oz,
                                               double oo, double dx, double dy, double dz, double& tmin, int& hit,
-                                              bool& tie) {
+                                              bool& tie, Wk& wk) {
+  wk.test(cnt);
   const int end = first + cnt;
   int k = first;
   for (; k + 1 < end; k += 2) {
@@ -532,9 +512,9 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
 // walk that enters a node when any lane of the wave may hit it before its current nearest t.
 // Evaluation order differs from scene order, which the result does not depend on: the nearest t
 // is a minimum, `hit` is its unique owner unless tied, and a tie is flagged whatever the order.
-template <bool CAM>
+template <bool CAM, typename Wk>
 __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double oy, double oz, double dx, double dy,
-                                            double dz, double& tmin, int& hit, bool& tie) {
+                                            double dz, double& tmin, int& hit, bool& tie, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
   const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
@@ -542,14 +522,15 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
   tmin = FARAWAY;
   hit = -1;
   tie = false;
-  nearest_range<CAM>(cg, 0, (int)sc[RTX_H_NALWAYS], ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
+  nearest_range<CAM>(cg, 0, (int)sc[RTX_H_NALWAYS], ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie, wk);
   const RaySlab rs = ray_slab(dx, dy, dz, oo);
   int i = 0;
   while (i < nn) {
     const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
+    wk.node();
     if (__ballot(node_may_hit(nd, ox, oy, oz, rs, tmin)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
-      if (cnt > 0) nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie);
+      if (cnt > 0) nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie, wk);
       ++i;
     } else {
       i = (int)nd[RTX_N_SKIP];
@@ -608,8 +589,9 @@ __device__ __forceinline__ void nearest_count_bvh(const cdouble* sc, double ox, 
 // unless some sphere is strictly nearer than the shape itself along the light direction. hs: the
 // wave-uniform shape of every lane (nsph when the lanes differ), whose own test cannot shadow it.
 // Callers guarantee t_self <= FARAWAY in every lane (an invalid test then never shadows).
+template <typename Wk>
 __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
-                                        double ly, double lz, double tself, int hs) {
+                                        double ly, double lz, double tself, int hs, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
   const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
@@ -618,6 +600,7 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
   for (int k = 0; k < nal; ++k) {
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
     if ((int)g0[RTX_G_IDX] == hs) continue;
+    wk.test(1);
     double b0, d0;
     bool k0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
@@ -629,9 +612,11 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
   int i = 0;
   while (i < nn) {
     const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
+    wk.node();
     if (__ballot(lit && node_may_hit(nd, qx, qy, qz, rs, tself)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
       if (cnt > 0) {
+        wk.test(cnt);
         const int first = (int)nd[RTX_N_FIRST], end = first + cnt;
         int k = first;
         for (; k + 1 < end; k += 2) {
@@ -666,9 +651,10 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
 
 // Nearest hit of ray (O, D) over all spheres; wave-uniform loop over sphere pairs, geometry through
 // the scalar cache. CAM: O is the camera (level 0), using the host-precomputed c.
-template <bool CAM, typename P>
+template <bool CAM, typename P, typename Wk>
 __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, double oy, double oz, double dx,
-                                            double dy, double dz, double& tmin, int& hit, bool& tie) {
+                                            double dy, double dz, double& tmin, int& hit, bool& tie, Wk& wk) {
+  wk.test(nsph);
   tmin = FARAWAY;
   hit = -1;
   tie = false;
@@ -821,11 +807,7 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   if (igain != 0.0) {
     const double af = fabs(va - 0.5) * 2.0;  // :204
     const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
-#ifdef RTX_ABL_SIN  // timing ablation only (wrong output)
-    const double ip = phase * 0.1;
-#else
     const double ip = sin_ref(phase);  // :211
-#endif
     const double hs = mh[RTX_M_HS], omhs = mh[RTX_M_1MHS];
     const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
     const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222
@@ -844,9 +826,10 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 // assembly (hit_color) and the reflection recursion (driven by the caller).
 // geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
 // same table (LDS copy or global).
-template <typename T, typename G>
+template <typename T, typename G, typename Wk>
 __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* tab, int nsph, int h, double ox,
-                                      double oy, double oz, double dx, double dy, double dz, double t, Hit& s) {
+                                      double oy, double oz, double dx, double dy, double dz, double t, Hit& s,
+                                      Wk& wk) {
   const T* gh = tab + h * RTX_GEOM_WORDS;
   const T* mh = tab + nsph * RTX_GEOM_WORDS + h * RTX_MAT_WORDS;
   const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73
@@ -862,6 +845,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   // Equivalent any-hit form: lit unless some sphere is strictly nearer than the shape itself.
   const double qq = dot3(qx, qy, qz, qx, qy, qz);
   const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
+  wk.test(1);
   bool lit = true;
   // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
   // shadows. The linear loop handles it exactly; the culling tree skips missing spheres, so such
@@ -871,20 +855,16 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
   const int h0 = __builtin_amdgcn_readfirstlane(h);
   const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
-#ifdef RTX_ABL_SHADOW  // timing ablation only (wrong output)
-  lit = tself > 1.0;
-  const int nshadow = 0;
-#else
   const bool culled = sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
-  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs);
+  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, wk);
   const int nshadow = culled ? 0 : nsph - (hs < nsph);
-#endif
   int j = 0;
   for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
     const int j0 = __builtin_amdgcn_readfirstlane(j + (j >= hs));
     const int j1 = __builtin_amdgcn_readfirstlane(j + 1 + (j + 1 >= hs));
     const G* g0 = geo + j0 * RTX_GEOM_WORDS;
     const G* g1 = geo + j1 * RTX_GEOM_WORDS;
+    wk.test(2);
     double b0, d0, b1, d1, t0, t1;
     bool k0, k1;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
@@ -898,6 +878,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   }
   if (lit && j < nshadow) {
     const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
+    wk.test(1);
     double b0, d0;
     bool k0;
     isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
@@ -922,11 +903,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   if (weighted || need_irid) {
     double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
     norm3(vx, vy, vz);  // :76 (towards the camera on every level)
-#ifdef RTX_ABL_SPEC  // timing ablation only (wrong output)
-    if (weighted) spec = vx * lx + vy;
-#else
     if (weighted) spec = specular(mh, g, nx, ny, nz, lx, ly, lz, vx, vy, vz);
-#endif
     if (need_irid) va = clip01(dot3(nx, ny, nz, vx, vy, vz));  // :201
   }
   s.dli = dli;
@@ -1050,7 +1027,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // overlaps the LDS staging of the scene table. DEEP (caps above 8 or none): chains still alive
 // after B levels are deferred with a resume record, and the continuation mode exists; the capped
 // instantiations compile none of it.
-template <int B, bool LDS, bool DEEP, bool LVL>
+template <int B, bool LDS, bool DEEP, bool LVL, bool STATS>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   const cdouble* sc = (const cdouble*)p.scene;
@@ -1090,11 +1067,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
   }
   const bool cam0 = (p.mode == 0);
-#ifdef RTX_WAVE_TIMES  // the wave-timing diagnostic borrows the stats buffer
-  unsigned long long* const st = nullptr;
-#else
-  unsigned long long* st = p.stats;
-#endif
+  // per-level counters: the stats instantiation only (the timed kernels compile none of it)
+  unsigned long long* const st = STATS ? p.stats : nullptr;
+  Work<STATS> wk;
   double ox = 0.0, oy = 0.0, oz = 0.0, dx = 0.0, dy = 0.0, dz = 1.0;
   // nearest hit of the current level's ray over all shapes (base.py:97-103): wave-uniform loop,
   // geometry via s_load
@@ -1119,14 +1094,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     if (sc[RTX_H_NNODES] != 0.0) {
       if (cam0) {
-        nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+        nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
       } else {
-        nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+        nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
       }
     } else if (cam0) {
-      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
     } else {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
     }
   }
   if constexpr (LDS) {
@@ -1168,9 +1143,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     Hit s;
     if constexpr (LDS) {
-      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, wk);
     } else {
-      shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s);
+      shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, wk);
     }
     const bool weighted = s.lit && s.g != 0.0;
     // the cap itself (absolute level; a continuation pass may run into a cap of 9 or 10)
@@ -1249,14 +1224,20 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_wave(st, RTX_S_WTRACE + kb + k + 1);
     }
     if (sc[RTX_H_NNODES] != 0.0) {
-      nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
     } else if constexpr (LDS) {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
     } else {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
     }
   }
 
+  if constexpr (STATS) {
+    if (st) {
+      stat_add(st, RTX_S_TESTS, wk.tests);
+      stat_add(st, RTX_S_NODES, wk.nodes);
+    }
+  }
   if (deferred) {
     // a tie (deep deferrals were appended with their resume record)
     if (!appended) append_deferred(p, deferred_entry(i, p.frame, rays_through, hits_through));
@@ -1308,8 +1289,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   write_out(p, i, cr, cg, cb);
 }
 
-template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>()>
-__global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? (B >= 5 ? RTX_B5_WAVES : RTX_LV_WAVES) : RTX_FAST_WAVES)) void k_render_fast(Params p0) {
+template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false>
+__global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : kLvWaves) : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
@@ -1327,15 +1308,11 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? (B >= 5 
     const double* src = p.scene + RTX_HDR_WORDS;
     for (int k = threadIdx.x; k < p.nsph * kSphWords; k += kFastBlock) lds_tab[k] = src[k];
   }
-#ifdef RTX_WAVE_TIMES  // diagnostic (tools/wave_times.py): per-wave start/end, 100 MHz clock
-  const int64_t wslot = RTX_S_WORDS + 2 * ((((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * kFastWaves + (threadIdx.x >> 6));
-  if (p.stats && p.n_fetch == 0 && (threadIdx.x & 63) == 0) p.stats[wslot] = __builtin_amdgcn_s_memrealtime();
-#endif
   if constexpr (DEEP) {
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
       for (int64_t t = blockIdx.x; t * kFastBlock < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP, LVL>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+        fast_tile<B, LDS, DEEP, LVL, STATS>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
     }
@@ -1366,16 +1343,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? (B >= 5 
     while (k < tiles_c) {
       const int t = c + k * nc;
       const int row = t / p.n_tiles_x;
-#ifdef RTX_WAVE_TIMES  // per-tile start/end, slot = tile in dispatch order
-      const uint64_t ts = __builtin_amdgcn_s_memrealtime();
-#endif
-      fast_tile<B, LDS, DEEP, LVL>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
-#ifdef RTX_WAVE_TIMES
-      if (p.stats && lane == 0) {
-        p.stats[RTX_S_WORDS + 2 * t] = ts;
-        p.stats[RTX_S_WORDS + 2 * t + 1] = __builtin_amdgcn_s_memrealtime();
-      }
-#endif
+      fast_tile<B, LDS, DEEP, LVL, STATS>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
       if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
@@ -1385,27 +1353,11 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? RTX_DEEP_WAVES : LVL ? (B >= 5 
     if (lane == 0 && v == dyn + waves_c - 1) atomicExch(ctr, 0u);
     return;
   }
-  if (p.n_tiles_x == 0) {  // one tile per block
-    // Bottom tile rows are dispatched first: they hold the ground and the spheres, whose pixels
-    // run long bounce chains, while sky rows finish at level 0 and so fill the end of the grid
-    // (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on the order.
-#ifdef RTX_FORWARD_ROWS
-    fast_tile<B, LDS, DEEP, LVL>(p, blockIdx.x, blockIdx.y, true, lds_tab);
-#else
-    fast_tile<B, LDS, DEEP, LVL>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
-#endif
-#ifdef RTX_WAVE_TIMES
-    if (p.stats && (threadIdx.x & 63) == 0) p.stats[wslot + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-    return;
-  }
-  // several tiles per block: tile t of the bottom-up row-major order, grid-stride (block b renders
-  // tiles b, b + G, ...: a bottom-half tile, then a lighter upper one)
-  const int nt = p.n_tiles_x * p.n_tiles_y;
-  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    const int row = t / p.n_tiles_x;
-    fast_tile<B, LDS, DEEP, LVL>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, t == (int)blockIdx.x, lds_tab);
-  }
+  // one tile per block. Bottom tile rows are dispatched first: they hold the ground and the
+  // spheres, whose pixels run long bounce chains, while sky rows finish at level 0 and so fill the
+  // end of the grid (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on
+  // the order.
+  fast_tile<B, LDS, DEEP, LVL, STATS>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1526,7 +1478,8 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     }
     if (st && d < RTX_S_LEVELS && d > hits_through) stat_add(st, RTX_S_HITS + d, 1);
     Hit s;
-    shade(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s);
+    Work<false> nowk;
+    shade(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, nowk);
     const bool weighted = s.lit && s.g != 0.0;
     bool descend = weighted && (B < 0 || d < B);
     if (descend && d + 1 >= p.stack_levels) {  // deeper than the stack: RecursionError on the host
@@ -1750,12 +1703,6 @@ inline void prof_next() {
   g_prof.on = false;
 }
 
-#ifndef RTX_CAPPED_MAX
-#define RTX_CAPPED_MAX RTX_FAST_MAX_BOUNCES  // caps rendered entirely by k_render_fast<cap>
-#endif
-#ifndef RTX_TILES_PER_BLOCK
-#define RTX_TILES_PER_BLOCK 1  // k_render_fast tiles per block (grid-stride loop when > 1)
-#endif
 
 int device_cus() {  // compute units of the current device (cached per device)
   static int cus[64] = {0};
@@ -1780,7 +1727,7 @@ int64_t workers_for(int64_t n, int max_bounces) {
   const size_t per = (size_t)stack_levels_for(max_bounces) * kFrameWords * sizeof(double);
   int64_t w = (int64_t)(kStackBudget / per);
   if (w > kMaxWorkers) w = kMaxWorkers;
-  const bool capped = max_bounces >= 0 && max_bounces <= RTX_CAPPED_MAX;
+  const bool capped = max_bounces >= 0 && max_bounces <= kCappedMax;
   const int64_t cap = capped ? kDeferredWorkers : kDeepWorkers;
   if (w > cap) w = cap;
   const int64_t need = ((n + 63) / 64) * 64;
@@ -1793,14 +1740,14 @@ size_t list_bytes(int64_t n) { return (size_t)n * sizeof(int64_t); }
 
 // resume records of deferral pass `pass`: only when chains are deferred for depth
 int64_t records_for(int64_t n, int max_bounces, int pass = 0) {
-  const bool capped = max_bounces >= 0 && max_bounces <= RTX_CAPPED_MAX;
+  const bool capped = max_bounces >= 0 && max_bounces <= kCappedMax;
   return capped ? 0 : records_cap(n, pass);
 }
 
 size_t round256(size_t b) { return (b + 255) / 256 * 256; }
 
 // Workspace: header | tile counters | list 1 | (deep chains:) lists 2 and 3 | records of level
-// RTX_DEEP_LEVELS, kDeepLevel2 and kDeepLevel3 | general-kernel stacks
+// kDeepLevels, kDeepLevel2 and kDeepLevel3 | general-kernel stacks
 struct WsLayout {
   size_t fetch, list1, list2, list3, rec1, rec2, rec3, stack, total;
 };
@@ -1814,7 +1761,7 @@ WsLayout ws_layout(int64_t n, int max_bounces) {
   w.list2 = w.list1 + round256(list_bytes(n));
   w.list3 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
   w.rec1 = w.list3 + (nrec ? round256(list_bytes(n)) : 0);
-  w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(RTX_DEEP_LEVELS) * sizeof(double));
+  w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(kDeepLevels) * sizeof(double));
   w.rec3 = w.rec2 + round256((size_t)nrec2 * rec_words(kDeepLevel2) * sizeof(double));
   w.stack = w.rec3 + round256((size_t)nrec3 * rec_words(kDeepLevel3) * sizeof(double));
   w.total = w.stack + (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
@@ -1842,16 +1789,24 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
   if (getenv("RTX_DEBUG_GRID"))
     fprintf(stderr, "persistent grid: %d blocks/CU x %d CUs -> %lld blocks, %d counters, %lld tiles\n", per_cu,
             device_cus(), (long long)blocks, p.n_fetch, (long long)nt);
-  static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "RTX_FETCH_COUNTERS must be a power of two");
   return dim3((unsigned)blocks);
 }
 
+// STATS: the instantiation with the per-level and executed-work counters (stats buffer given)
+template <int B, bool DEEP, bool LVL, bool STATS>
+void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
+  const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
+  if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL, STATS>, lds, p);
+  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS>), grid, dim3(kFastBlock), (uint32_t)lds, s,
+                        prof_event(0), prof_event(1), 0u, p);
+}
 template <int B, bool DEEP, bool LVL>
 void launch_fast_lds(Params& p, dim3 grid, hipStream_t s) {
-  const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
-  if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL>, lds, p);
-  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL>), grid, dim3(kFastBlock), (uint32_t)lds, s, prof_event(0),
-                        prof_event(1), 0u, p);
+  if (p.stats) {
+    launch_fast_lds_s<B, DEEP, LVL, true>(p, grid, s);
+  } else {
+    launch_fast_lds_s<B, DEEP, LVL, false>(p, grid, s);
+  }
 }
 
 template <int B, bool DEEP = false>
@@ -1859,7 +1814,7 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
   Params p = p0;
   if (p.nsph <= kLdsMaxSpheres) {
     if constexpr (DEEP) {
-      if (RTX_LEVELS_IN_LDS && p.nsph <= RTX_DEEP_LV_MAX_SPHERES) {
+      if (kLevelsInLds && p.nsph <= kDeepLvMaxSpheres) {
         launch_fast_lds<B, true, true>(p, grid, s);
       } else {
         launch_fast_lds<B, true, false>(p, grid, s);
@@ -1868,14 +1823,20 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
       launch_fast_lds<B, false, levels_in_lds<B, true, false>()>(p, grid, s);
     }
   } else {
-    if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP>, 0, p);
-    hipExtLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0u, s, prof_event(0),
-                          prof_event(1), 0u, p);
+    if (p.stats) {
+      if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP, false, true>, 0, p);
+      hipExtLaunchKernelGGL((k_render_fast<B, false, DEEP, false, true>), grid, dim3(kFastBlock), 0u, s,
+                            prof_event(0), prof_event(1), 0u, p);
+    } else {
+      if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP>, 0, p);
+      hipExtLaunchKernelGGL((k_render_fast<B, false, DEEP>), grid, dim3(kFastBlock), 0u, s, prof_event(0),
+                            prof_event(1), 0u, p);
+    }
   }
 }
 
-// caps above RTX_CAPPED_MAX or none: RTX_DEEP_LEVELS levels, longer chains deferred with a record
-void launch_fast_deep(const Params& p, dim3 grid, hipStream_t s) { launch_fast_b<RTX_DEEP_LEVELS, true>(p, grid, s); }
+// caps above kCappedMax or none: kDeepLevels levels, longer chains deferred with a record
+void launch_fast_deep(const Params& p, dim3 grid, hipStream_t s) { launch_fast_b<kDeepLevels, true>(p, grid, s); }
 
 void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
   switch (B) {
@@ -1915,25 +1876,20 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack = (double*)(p.ws + lay.stack);
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
-  const bool capped = p.max_bounces >= 0 && p.max_bounces <= RTX_CAPPED_MAX;
+  const bool capped = p.max_bounces >= 0 && p.max_bounces <= kCappedMax;
   p.n_workers = workers_for(n_all, p.max_bounces);
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
     dim3 grid;
     const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kFastBlock - 1) / kFastBlock);
     const int ty = p.mode == 0 ? (p.n_rows + kTileH - 1) / kTileH : 1;
-    const int64_t nt = (int64_t)tx * ty;
     p.n_fetch = 0;
-    if (p.nsph >= RTX_PERSIST_MIN_SPHERES && p.mode == 0 && p.n_frames == 1) {
+    if (p.nsph >= kPersistMinSpheres && p.mode == 0 && p.n_frames == 1) {
       p.n_tiles_x = (p.width + kWaveW - 1) / kWaveW;  // wave tiles
       p.n_tiles_y = (p.n_rows + kWaveH - 1) / kWaveH;
       p.fetch = (uint32_t*)(p.ws + lay.fetch);
       p.n_fetch = kMaxFetch;  // launch_fast_b sizes the grid and the counters in use
       grid = dim3(1);
-    } else if (RTX_TILES_PER_BLOCK > 1 && nt > RTX_TILES_PER_BLOCK) {
-      p.n_tiles_x = tx;
-      p.n_tiles_y = ty;
-      grid = dim3((unsigned)((nt + RTX_TILES_PER_BLOCK - 1) / RTX_TILES_PER_BLOCK), 1, (unsigned)p.n_frames);
     } else {
       p.n_tiles_x = p.n_tiles_y = 0;
       grid = dim3((unsigned)tx, (unsigned)ty, (unsigned)p.n_frames);
@@ -1941,7 +1897,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     p.dlist = list1;
     p.dcount = hdr + RTX_WS_COUNT;
     p.drec = capped ? nullptr : rec1;
-    p.drec_level = RTX_DEEP_LEVELS;
+    p.drec_level = kDeepLevels;
     prof_mark(0, s);
     if (capped) {
       launch_fast(p.max_bounces, p, grid, s);
@@ -1955,9 +1911,9 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.in_list = list1;
   p.in_count = hdr + RTX_WS_COUNT;
   p.in_rec = capped ? nullptr : rec1;
-  p.in_level = RTX_DEEP_LEVELS;
+  p.in_level = kDeepLevels;
   if (!capped && p.n_frames == 1) {
-    // continuation passes: chains deferred for depth go on for RTX_DEEP_LEVELS + 1 more levels in
+    // continuation passes: chains deferred for depth go on for kDeepLevels + 1 more levels in
     // the register-resident kernel, twice; ties and what is still alive after them go to the
     // general kernel
     uint64_t* const lists[2] = {list2, (uint64_t*)(p.ws + lay.list3)};

@@ -437,6 +437,7 @@ class HipRenderer(Renderer):
         hits = s[L.S_HITS:L.S_HITS + L.S_LEVELS]
         last = max([i + 1 for i, v in enumerate(rays) if v] or [0])
         return {"pixels": s[L.S_PIXELS], "deferred": s[L.S_DEFERRED], "ties": s[L.S_TIES],
+                "sphere_tests": s[L.S_TESTS], "node_tests": s[L.S_NODES],
                 "rays": rays[:last], "hits": hits[:last],
                 "waves_traced": s[L.S_WTRACE:L.S_WTRACE + last], "waves_shaded": s[L.S_WSHADE:L.S_WSHADE + last]}
 

@@ -1,0 +1,60 @@
+"""Build librtx_hip.so variants for tools/ab.py (A/B timing on identical output).
+
+    python tools/ab_build.py OUT.so [--set kName=VALUE ...] [--rev GIT_REV] [--patch FILE.py]
+
+The shipped kernel has no tuning macros: its tuning values are ``constexpr`` lines in
+``csrc/rtx_kernels.hip``. A variant rewrites those lines (``--set kLvWaves=4``), takes the source of
+another revision (``--rev HEAD~3``: the baseline of an A/B), or applies a Python patch script that
+edits the source text (``--patch``: ``def patch(src: str) -> str``), and compiles it with the
+library's own flags next to the original (so its relative #include resolves).
+"""
+
+import argparse
+import re
+import runpy
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+from python_ray_tracer_amd import _build  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--set", action="append", default=[], help="kName=VALUE (a constexpr tuning line)")
+    ap.add_argument("--rev", default=None, help="git revision of csrc/rtx_kernels.hip to build")
+    ap.add_argument("--patch", default=None, help="python file defining patch(src) -> src")
+    ap.add_argument("--flag", action="append", default=[], help="extra hipcc flag")
+    a = ap.parse_args()
+    rel = _build.SRC.relative_to(REPO)
+    if a.rev:
+        src = subprocess.run(["git", "show", f"{a.rev}:{rel}"], cwd=REPO, check=True, capture_output=True,
+                             text=True).stdout
+    else:
+        src = _build.SRC.read_text()
+    for kv in a.set:
+        name, val = kv.split("=", 1)
+        pat = re.compile(rf"^(constexpr\s+\w+\s+{re.escape(name)}\s*=\s*)([^;]+)(;)", re.M)
+        src, n = pat.subn(lambda m: m.group(1) + val + m.group(3), src)
+        if n != 1:
+            raise SystemExit(f"--set {name}: {n} matching constexpr lines")
+    if a.patch:
+        src = runpy.run_path(a.patch)["patch"](src)
+    tmp = _build.SRC.with_name(f"_ab_{Path(a.out).stem}.hip")
+    tmp.write_text(src)
+    try:
+        out = Path(a.out).resolve()
+        out.parent.mkdir(parents=True, exist_ok=True)
+        cmd = [_build.hipcc(), *_build.HIPCC_FLAGS, *a.flag, "-o", str(out), str(tmp)]
+        subprocess.run(cmd, check=True, cwd=str(REPO))
+    finally:
+        tmp.unlink(missing_ok=True)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()
