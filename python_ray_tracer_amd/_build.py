@@ -13,6 +13,8 @@ REPO = PKG.parent
 SRC = PKG / "csrc" / "rtx_kernels.hip"
 HDR = REPO / "include" / "rtx_hip.h"
 LIB = PKG / "librtx_hip.so"
+OPS_SRC = PKG / "csrc" / "rt_ops.cpp"
+OPS_LIB = PKG / "librt_ops.so"
 
 # -ffp-contract=off: NumPy never fuses a*b+c, and FMA contraction would move linspace / checker
 # boundaries. No fast-math: sqrt and division stay correctly rounded.
@@ -51,5 +53,36 @@ def build_library(force: bool = False, extra_flags=(), out: Path | None = None, 
     return out
 
 
+def ops_flags() -> list:
+    """Compile/link flags of the TORCH_LIBRARY(rt) op library against the installed torch (the
+    include and library paths torch.utils.cpp_extension would use), linked to librtx_hip.so."""
+    import torch
+    import torch.utils.cpp_extension as ce
+
+    inc = [f"-I{p}" for p in ce.include_paths(device_type="cuda")]
+    libdirs = [p for p in ce.library_paths(device_type="cuda") if Path(p).exists()]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return (["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+             "-Wno-unused-result", "-Wno-deprecated-declarations"] + inc + [f"-L{p}" for p in libdirs]
+            + [f"-L{PKG}", "-lrtx_hip", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+               "-Wl,-rpath,$ORIGIN"] + [f"-Wl,-rpath,{p}" for p in libdirs])
+
+
+def build_ops(force: bool = False, verbose: bool = False) -> Path:
+    """librt_ops.so: the PyTorch custom ops rt::* (csrc/rt_ops.cpp) over the C ABI. Host code only,
+    compiled by hipcc as C++ (HIP runtime headers for c10::hip)."""
+    if not force and OPS_LIB.exists() and all(p.stat().st_mtime <= OPS_LIB.stat().st_mtime
+                                              for p in (OPS_SRC, HDR, LIB, Path(__file__))):
+        return OPS_LIB
+    tmp = OPS_LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), "-x", "c++", *ops_flags(), "-o", str(tmp), str(OPS_SRC)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=str(REPO))
+    os.replace(tmp, OPS_LIB)
+    return OPS_LIB
+
+
 if __name__ == "__main__":
     print(build_library(force=True, verbose=True))
+    print(build_ops(force=True, verbose=True))

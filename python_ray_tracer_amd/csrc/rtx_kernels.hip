@@ -50,7 +50,6 @@ constexpr int kBlock = 256;   // threads per block of the elementwise boundary k
 // tools/ab_build.py builds variants by rewriting these lines) ----
 constexpr int kWaveW = 8;       // pixels per wave row: a wave renders a kWaveW x (64 / kWaveW) tile
 constexpr int kFastWaves = 4;   // waves per k_render_fast block (1, 2 or 4)
-constexpr int kBlockWavesX = 2; // of them side by side in the block tile (the rest stacked)
 // k_render_fast single-frame launches of scenes with at least this many spheres: persistent waves
 // fetching wave tiles (A/B: 65 spheres -14%, 17 spheres +-0, 3-16 spheres without the culling tree
 // +12%: their tiles are short, so the ramp-up of the fetch counters and the drain cost more than
@@ -78,7 +77,7 @@ constexpr int kWaveH = 64 / kWaveW;
 static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
 static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "kMaxFetch must be a power of two");
 constexpr int kFastBlock = 64 * kFastWaves;
-constexpr int kWavesX = kFastWaves < kBlockWavesX ? kFastWaves : kBlockWavesX;  // block tile: kWavesX x kWavesY waves
+constexpr int kWavesX = kFastWaves == 1 ? 1 : 2;  // block tile: kWavesX x kWavesY waves
 constexpr int kWavesY = kFastWaves / kWavesX;
 constexpr int kTileW = kWavesX * kWaveW;
 constexpr int kTileH = kWavesY * kWaveH;
@@ -1030,7 +1029,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // instantiations compile none of it.
 template <int B, bool LDS, bool DEEP, bool LVL, bool STATS>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
-                                          bool wave_tile = false, double* stage = nullptr) {
+                                          bool wave_tile = false) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
@@ -1108,14 +1107,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   if constexpr (LDS) {
     if (first) __syncthreads();
   }
-  // stage (one-tile-per-block camera launches with LDS level slots): the colour goes to this lane's
-  // level-0 slot and its written flag to its level-0 key slot instead of HBM; k_render_fast writes
-  // the block tile out after a barrier (whole row segments per store instruction)
-  int* const sflag = stage ? (int*)(stage + level_lds_slots<DEEP>(B) * 4 * kFastBlock) : nullptr;
-  if (!active) {
-    if (stage) sflag[threadIdx.x] = 0;
-    return;
-  }
+  if (!active) return;
 
   // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level), or,
   // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
@@ -1249,7 +1241,6 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   if (deferred) {
     // a tie (deep deferrals were appended with their resume record)
     if (!appended) append_deferred(p, deferred_entry(i, p.frame, rays_through, hits_through));
-    if (stage) sflag[lt] = 0;
     if (st && !rin) stat_add(st, RTX_S_DEFERRED, 1);
     return;
   }
@@ -1295,27 +1286,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
                 cr, cg, cb, cr, cg, cb);
     }
   }
-  if (stage) {  // this lane's own level-0 slot: its fold (above) has read every level it holds
-    stage[lt] = cr;
-    stage[kFastBlock + lt] = cg;
-    stage[2 * kFastBlock + lt] = cb;
-    sflag[lt] = 1;
-  } else {
-    write_out(p, i, cr, cg, cb);
-  }
-}
-
-// The block tile staged by fast_tile, written out after the block's barrier: thread t takes pixel
-// (t % kTileW, t / kTileW) of the tile, so consecutive lanes store consecutive pixels of one frame
-// row (kTileW * 4 bytes contiguous per float32 plane and store instruction, instead of the 8-pixel
-// row segments of an 8x8 wave tile).
-__device__ __forceinline__ void write_block_tile(const Params& p, int bx, int by, const double* stage,
-                                                 const int* sflag) {
-  const int x = threadIdx.x % kTileW, y = threadIdx.x / kTileW;
-  const int src = ((y / kWaveH) * kWavesX + (x / kWaveW)) * 64 + (y % kWaveH) * kWaveW + (x % kWaveW);
-  const int col = bx * kTileW + x, lr = by * kTileH + y;
-  if (col < p.width && lr < p.n_rows && sflag[src])
-    write_out(p, (int64_t)lr * p.width + col, stage[src], stage[kFastBlock + src], stage[2 * kFastBlock + src]);
+  write_out(p, i, cr, cg, cb);
 }
 
 template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false>
@@ -1386,17 +1357,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
   // spheres, whose pixels run long bounce chains, while sky rows finish at level 0 and so fill the
   // end of the grid (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on
   // the order.
-  const int by = gridDim.y - 1 - blockIdx.y;
-  if constexpr (LVL) {
-    if (p.mode == 0) {
-      double* const stage = const_cast<double*>(lds_tab) + p.nsph * kSphWords;  // the level slots
-      fast_tile<B, LDS, DEEP, LVL, STATS>(p, blockIdx.x, by, true, lds_tab, false, stage);
-      __syncthreads();
-      write_block_tile(p, blockIdx.x, by, stage, (const int*)(stage + level_lds_slots<DEEP>(B) * 4 * kFastBlock));
-      return;
-    }
-  }
-  fast_tile<B, LDS, DEEP, LVL, STATS>(p, blockIdx.x, by, true, lds_tab);
+  fast_tile<B, LDS, DEEP, LVL, STATS>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 }
 
 // ------------------------------------------------------------------------------------------
