@@ -1,0 +1,108 @@
+"""torch.ops.rt (the TORCH_LIBRARY surface, csrc/rt_ops.cpp) on the GPU: every op returns exactly
+what the ctypes path of HipRenderer returns for the same inputs (both call the same C entry
+points), runs on the current stream, and rejects bad tensors with RuntimeError."""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import numpy_oracle as O
+from python_ray_tracer_amd import scenes, tiling
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import python_ray_tracer_amd.ops  # noqa: F401
+    from python_ray_tracer_amd.infrastructure import hip as H
+
+    return H
+
+
+def test_render_tile_trace_match_hiprenderer(env):
+    H = env
+    spec = scenes.random_spec(16, 2, 200, 117)
+    scene = scenes.build_scene(spec)
+    for B, bl in ((3, 3), (None, -1), (8, 8)):
+        r = H.HipRenderer(max_bounces=B, color_dtype=torch.float32)
+        blob, S = r.scene_blob(scene)
+        ws = torch.zeros(torch.ops.rt.workspace_bytes(200 * 117, bl), dtype=torch.uint8, device="cuda")
+        got = torch.ops.rt.render_tile(blob, S, 200, 117, 1, 1, 0, bl, 0, ws)
+        assert got.dtype == torch.float32 and got.shape == (3, 200 * 117)
+        assert torch.equal(got, r.render(scene).data), B
+        # a row tile, uint8 and float64
+        assert torch.equal(torch.ops.rt.render_tile(blob, S, 200, 117, 8, 3, 1, bl, 2, ws),
+                           r.render_tile(scene, 8, 3, 1, out="u8"))
+        r64 = H.HipRenderer(max_bounces=B)
+        assert torch.equal(torch.ops.rt.render_tile(blob, S, 200, 117, 8, 3, 2, bl, 1, ws), r64.render_tile(scene, 8, 3, 2))
+        # per-level counters through the optional stats tensor
+        st = torch.zeros(264, dtype=torch.int64, device="cuda")
+        torch.ops.rt.render_tile(blob, S, 200, 117, 1, 1, 0, bl, 0, ws, st)
+        ost = O.TraceStats()
+        O.render(O.scene_from_spec(spec), B, stats=ost)
+        assert st[8:8 + len(ost.rays)].tolist() == ost.rays
+    # trace: shared and per-ray origins
+    sc = O.scene_from_spec(spec)
+    d = np.stack(O.ray_directions(sc.cam, 200, 117))
+    D = torch.from_numpy(d).cuda()
+    r = H.HipRenderer(max_bounces=3)
+    blob, S = r.scene_blob(scene)
+    ws = torch.zeros(torch.ops.rt.workspace_bytes(D.shape[1], 3), dtype=torch.uint8, device="cuda")
+    org = torch.tensor(sc.cam, dtype=torch.float64, device="cuda")
+    got = torch.ops.rt.trace(blob, S, org, D, 3, 1, ws)
+    assert np.abs(got.cpu().numpy() - O.render(sc, 3)).max() <= 1e-12
+    O2 = org[:, None].expand(3, D.shape[1]).contiguous() + 0.01
+    assert torch.equal(torch.ops.rt.trace(blob, S, O2, D, 3, 1, ws),
+                       r.raytrace_scene(H.HipVector3D(*O2), H.HipVector3D(*D), scene).data)
+
+
+def test_intersect_quantize_assemble(env):
+    H = env
+    from python_ray_tracer_amd.infrastructure.hip.scene_pack import sphere_geometry
+
+    for k in json.loads((GOLDEN / "intersect_kat.json").read_text()):
+        g = torch.from_numpy(sphere_geometry(tuple(float(v) for v in k["center"]), k["radius"])).cuda()
+        t = torch.ops.rt.intersect(g, torch.tensor(k["origin"], dtype=torch.float64, device="cuda"),
+                                   torch.tensor(k["dir"], dtype=torch.float64, device="cuda").reshape(3, 1))
+        assert float(t[0]) == k["t"], k["label"]
+    vals = torch.linspace(-0.5, 1.5, 3001, dtype=torch.float64, device="cuda")
+    c = torch.stack([vals, vals.flip(0), vals.roll(5)])
+    q = torch.ops.rt.quantize_u8(c)
+    assert np.array_equal(q.cpu().numpy().reshape(1, -1, 3), O.to_uint8(c.cpu().numpy(), 3001, 1))
+    spec = scenes.readme_spec(96, 53)
+    scene = scenes.build_scene(spec)
+    r = H.HipRenderer(max_bounces=3, color_dtype=torch.float32)
+    P, rb = 3, 4
+    n = tiling.part_len(53, 96, rb, P, 4)
+    buf = torch.zeros((P, n), dtype=torch.float32, device="cuda")
+    for p in range(P):
+        shp = tiling.tile_shape(53, 96, rb, P, p)
+        r.render_tile(scene, rb, P, p, into=buf[p, :3 * shp[1]].view(shp))
+    assert torch.equal(torch.ops.rt.assemble_rows(buf, 96, 53, rb, 0), r.render(scene).data)
+
+
+def test_op_argument_checks(env):
+    H = env
+    scene = scenes.build_scene(scenes.readme_spec(32, 18))
+    r = H.HipRenderer(max_bounces=3)
+    blob, S = r.scene_blob(scene)
+    ws = torch.zeros(torch.ops.rt.workspace_bytes(32 * 18, 3), dtype=torch.uint8, device="cuda")
+    with pytest.raises(RuntimeError, match="workspace too small"):
+        torch.ops.rt.render_tile(blob, S, 32, 18, 1, 1, 0, 3, 0, ws[:100])
+    with pytest.raises(RuntimeError, match="must be Double"):
+        torch.ops.rt.render_tile(blob.float(), S, 32, 18, 1, 1, 0, 3, 0, ws)
+    with pytest.raises(RuntimeError, match="too short"):
+        torch.ops.rt.render_tile(blob, S + 40, 32, 18, 1, 1, 0, 3, 0, ws)
+    with pytest.raises(RuntimeError, match="geometry"):
+        torch.ops.rt.render_tile(blob, S, 32, 18, 1, 2, 2, 3, 0, ws)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        torch.ops.rt.quantize_u8(torch.zeros(4, 3, device="cuda").t())
+    D = torch.zeros(3, 10, dtype=torch.float64, device="cuda")
+    with pytest.raises(RuntimeError, match="origins"):
+        torch.ops.rt.trace(blob, S, torch.zeros(3, 9, dtype=torch.float64, device="cuda"), D, 3, 0, ws)

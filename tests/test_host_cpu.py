@@ -273,3 +273,31 @@ def test_vector_algebra_matches_reference_expressions(backend):
         z = np.zeros(33)
         np.place(z, cond, np.extract(cond, w))
         assert np.array_equal(arr(g), z)
+
+
+def test_torch_ops_registered_and_checked_on_host():
+    """torch.ops.rt (csrc/rt_ops.cpp, TORCH_LIBRARY over the C ABI) loads without a GPU; its size
+    query equals the C ABI's; host tensors, wrong dtypes and short workspaces raise RuntimeError
+    (TORCH_CHECK) before anything is launched."""
+    import python_ray_tracer_amd.ops as ops
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    lib = L.load()
+    for name in ops.OPS:
+        assert hasattr(torch.ops.rt, name), name
+    for n, B in ((1, 0), (2073600, 3), (33177600, 5), (1000, -1)):
+        assert torch.ops.rt.workspace_bytes(n, B) == lib.rtx_workspace_bytes(n, B)
+    blob = torch.zeros(200, dtype=torch.float64)
+    ws = torch.zeros(64, dtype=torch.uint8)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.render_tile(blob, 3, 8, 8, 1, 1, 0, 3, 0, ws)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.trace(blob, 3, torch.zeros(3, dtype=torch.float64), torch.zeros(3, 5, dtype=torch.float64), 3, 0,
+                           ws)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.intersect(torch.zeros(8, dtype=torch.float64), torch.zeros(3, dtype=torch.float64),
+                               torch.zeros(3, 5, dtype=torch.float64))
+    with pytest.raises(RuntimeError):
+        torch.ops.rt.quantize_u8(torch.zeros(3, 4))
+    with pytest.raises(RuntimeError):
+        torch.ops.rt.assemble_rows(torch.zeros(2, 64, dtype=torch.uint8), 4, 4, 1, 2)
