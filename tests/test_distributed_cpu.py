@@ -98,3 +98,15 @@ def test_row_tiles_gather_equals_single_frame(world, row_block):
         assert set().union(*shards) == set(range(8))
         for r in range(world):
             assert shards[r] == {k for k in range(8) if k % world == r}
+
+
+def test_row_tiled_cpu_baseline_runs():
+    """oracle/row_tiled.py (bench.py's all-cores CPU baseline): whole frames through
+    render_frame_distributed, and the tile-sample mode of the big configs."""
+    from oracle import row_tiled
+
+    spec = scenes.readme_spec(48, 27)
+    full = row_tiled.time_row_tiled(spec, 3, 2, frames=2)
+    assert len(full["times"]) == 2 and full["pixels"] == [48 * 27] * 2
+    part = row_tiled.time_row_tiled(spec, 3, 2, frames=2, sub=2, row_block=4)
+    assert sum(part["pixels"]) == 48 * 27  # two steps cover the two halves of a 4-way split
