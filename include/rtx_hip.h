@@ -13,6 +13,7 @@
  *                          of the frame for the multi-GPU path (application.py:43-52 gains it)
  *   rtx_trace_rays      <- NumpyRenderer.raytrace_scene(ray_origin, dirs, scene) for an arbitrary
  *                          batch of rays                      (base.py:91-121)
+ *   rtx_shade_hits      <- NumpyShader.create (the Shader plugin, shader.py:63-112 / application.py:35-40)
  *   rtx_ray_directions  <- NumpyRenderer.get_ray_directions  (base.py:123-141)
  *   rtx_sphere_intersect<- NumpySphere.intersect             (shape.py:28-51)
  *   rtx_quantize_u8     <- NumpyRenderer.save_image's (255*clip(c,0,1)).astype(uint8)
@@ -222,6 +223,16 @@ int rtx_render_frames(const double* scenes, int64_t scene_stride, int n_frames, 
  * shared origin (origin_stride == 0, 3 doubles); dirs: [3][n]. */
 int rtx_trace_rays(const double* scene, int n_spheres, const double* origins, int64_t origin_stride,
                    const double* dirs, int64_t n, int max_bounces, void* out, int out_kind,
+                   void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
+
+/* NumpyShader.create(shape, scene, ray_origin, dirs, distance, ray_tracer) (shader.py:63-112): the
+ * colour of n rays that hit sphere `shape` at distances t[n] — P = O + D*t, shadow, diffuse, dome,
+ * specular, iridescence, and the reflection recursion through raytrace_scene up to max_bounces
+ * (the reflected rays are level 1; -1 = unbounded). The shape is taken as hit whether or not it is
+ * the nearest, as create shades what it is handed. Same origins/dirs layout as rtx_trace_rays;
+ * out_kind colour or u8; workspace rtx_workspace_bytes(n, max_bounces). */
+int rtx_shade_hits(const double* scene, int n_spheres, int shape, const double* origins, int64_t origin_stride,
+                   const double* dirs, const double* t, int64_t n, int max_bounces, void* out, int out_kind,
                    void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
 
 /* get_ray_directions (base.py:123-141) for the same row tiling: dirs_out [3][width*n_local_rows]. */

@@ -108,13 +108,16 @@ typedef const double __attribute__((address_space(4))) cdouble;
 struct Params {
   const double* scene;
   int nsph;
-  int mode;  // 0: camera rays, 1: explicit rays, 2: continuation of deferred chains (in_list)
+  int mode;  // 0: camera rays, 1: explicit rays, 2: continuation of deferred chains (in_list),
+             // 3: explicit rays whose level-0 hit is given (hit_shape at hit_t: Shader.create)
   // camera mode
   int width, height, row_block, n_parts, part, n_rows;
   // explicit-ray mode
   const double* org;
   int64_t org_stride;
   const double* dir;
+  const double* hit_t;  // mode 3: level-0 distance per ray
+  int hit_shape;        // mode 3: the shape every ray hit
   // common
   int64_t n;  // rays in this launch (= width * n_rows in camera mode)
   int max_bounces;
@@ -1047,7 +1050,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     lr = wave_tile ? by * kWaveH + (lane / kWaveW) : by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
-  } else if (!DEEP || p.mode == 1) {
+  } else if (!DEEP || p.mode == 1 || p.mode == 3) {
     i = (int64_t)bx * kFastBlock + threadIdx.x;
     active = i < p.n;
   } else {  // continuation: entry `item` of in_list
@@ -1092,7 +1095,10 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         stat_wave(st, RTX_S_WTRACE + kb);
       }
     }
-    if (sc[RTX_H_NNODES] != 0.0) {
+    if (p.mode == 3) {  // NumpyShader.create: the hit is given (shader.py:63-73)
+      tmin = p.hit_t[i];
+      hit = p.hit_shape;
+    } else if (sc[RTX_H_NNODES] != 0.0) {
       if (cam0) {
         nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
       } else {
@@ -1386,7 +1392,8 @@ struct Stack {
 template <typename Stk>
 __device__ void trace_general(const Params& p, const Stk& S, double ox0, double oy0, double oz0, double dx0,
                               double dy0, double dz0, double& cr, double& cg, double& cb, int rays_through,
-                              int hits_through, const double* rec = nullptr) {
+                              int hits_through, const double* rec = nullptr, int h_given = -1,
+                              double t_given = 0.0) {
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const double* tab = p.scene + RTX_HDR_WORDS;
@@ -1425,7 +1432,11 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       if (st && d < RTX_S_LEVELS && d > rays_through) stat_add(st, RTX_S_RAYS + d, 1);
       tmin = FARAWAY;
       int nh = 0, first = nsph;
-      if (sc[RTX_H_NNODES] != 0.0 && nsph >= kGeneralTreeMin) {
+      if (d == 0 && h_given >= 0) {  // Shader.create's ray: the level-0 hit is given
+        tmin = t_given;
+        nh = 1;
+        first = h_given;
+      } else if (sc[RTX_H_NNODES] != 0.0 && nsph >= kGeneralTreeMin) {
         nearest_count_bvh(sc, ox, oy, oz, oo, dx, dy, dz, tmin, nh, first);
       } else {
         for (int s = 0; s < nsph; ++s) {
@@ -1440,7 +1451,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
         }
       }
       if (st && nh > 1 && d > rays_through) stat_add(st, RTX_S_TIES, 1);
-      left = tmin != FARAWAY ? nh : 0;  // (nearest != FARAWAY) & (t == nearest), base.py:102-103
+      left = (tmin != FARAWAY || (d == 0 && h_given >= 0)) ? nh : 0;  // (nearest != FARAWAY) & (t == nearest), base.py:102-103
       S.at(d, F_TMIN) = tmin;
       S.at(d, F_LEFT) = (double)left;
       S.at(d, F_AR) = 0.0; S.at(d, F_AG) = 0.0; S.at(d, F_AB) = 0.0;  // NumpyRGBColor(0, 0, 0)
@@ -1541,8 +1552,10 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
           double ox = 0.0, oy = 0.0, oz = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
           if (!resume) load_ray(q, i, ox, oy, oz, dx, dy, dz);
           double cr, cg, cb;
+          const bool given = q.mode == 3;
           trace_general(q, S, ox, oy, oz, dx, dy, dz, cr, cg, cb, rays_through, hits_through,
-                        resume ? p.in_rec + item * rec_words(p.in_level) : nullptr);
+                        resume ? p.in_rec + item * rec_words(p.in_level) : nullptr, given ? q.hit_shape : -1,
+                        given ? q.hit_t[i] : 0.0);
           write_out(q, i, cr, cg, cb);
           todo = false;
         }
@@ -2070,6 +2083,29 @@ int rtx_trace_rays(const double* scene, int n_spheres, const double* origins, in
   p.org = origins;
   p.org_stride = origin_stride;
   p.dir = dirs;
+  p.n = n;
+  p.max_bounces = max_bounces;
+  p.out = out;
+  p.out_kind = out_kind;
+  p.stats = (unsigned long long*)stats;
+  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int rtx_shade_hits(const double* scene, int n_spheres, int shape, const double* origins, int64_t origin_stride,
+                   const double* dirs, const double* t, int64_t n, int max_bounces, void* out, int out_kind,
+                   void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream) {
+  if (!origins || !dirs || !t) return fail(RTX_E_ARG, "null ray pointer%s", "");
+  if (origin_stride != 0 && origin_stride != n) return fail(RTX_E_ARG, "origin_stride must be 0 or n%s", "");
+  if (shape < 0 || shape >= n_spheres) return fail(RTX_E_ARG, "shape index out of range%s (%lld)", "", shape);
+  Params p{};
+  p.scene = scene;
+  p.nsph = n_spheres;
+  p.mode = 3;
+  p.org = origins;
+  p.org_stride = origin_stride;
+  p.dir = dirs;
+  p.hit_t = t;
+  p.hit_shape = shape;
   p.n = n;
   p.max_bounces = max_bounces;
   p.out = out;

@@ -71,6 +71,7 @@ EXPORTS = (
     "rtx_profile_sample",
     "rtx_selftest_math",
     "rtx_assemble_rows",
+    "rtx_shade_hits",
 )
 
 _c_void_p = ctypes.c_void_p
@@ -95,6 +96,8 @@ _SIGS = {
     "rtx_profile_collect": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
     "rtx_profile_sample": (_i32, [_i32]),
     "rtx_selftest_math": (_i32, [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "rtx_shade_hits": (_i32, [_c_void_p, _i32, _i32, _c_void_p, _i64, _c_void_p, _c_void_p, _i64, _i32, _c_void_p,
+                              _i32, _c_void_p, _size, _c_void_p, _c_void_p]),
     "rtx_assemble_rows": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
 }
 

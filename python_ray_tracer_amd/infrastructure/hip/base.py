@@ -374,6 +374,38 @@ class HipRenderer(Renderer):
         self._check_status(ws)
         return res
 
+    def shade_hits(self, shape, scene, ray_origin, dirs, distance) -> torch.Tensor:
+        """NumpyShader.create of ``shape``'s shader for rays hitting ``shape`` at ``distance``
+        (shader.py:63-112, rtx_shade_hits); the reflected rays are level 1 of this renderer's
+        bounce cap. Returns [3, n] colour."""
+        si = next((k for k, s in enumerate(scene.shapes) if s is shape), None)
+        if si is None:  # scene.shapes.index(shape) in _calculate_shadow (shader.py:126)
+            raise ValueError("shape is not in scene.shapes")
+        blob, S = self.scene_blob(scene)
+        D = _as_vector(dirs).to_tensor(self.device)
+        if D.dim() != 2:
+            D = D.reshape(3, 1)
+        n = D.shape[1]
+        O = _as_vector(ray_origin).to_tensor(self.device, n)
+        stride = 0 if O.dim() == 1 else n
+        if stride and O.shape[1] != n:
+            raise ValueError(f"origins ({O.shape[1]}) and directions ({n}) differ in length")
+        t = distance if _is_tensor(distance) else torch.from_numpy(np.asarray(distance, dtype=np.float64))
+        t = t.to(device=self.device, dtype=torch.float64).reshape(-1)
+        if t.numel() == 1 and n > 1:
+            t = t.expand(n)
+        t = t.contiguous()
+        if t.numel() != n:
+            raise ValueError(f"distance ({t.numel()}) and directions ({n}) differ in length")
+        res = torch.empty((3, n), dtype=self.color_dtype, device=self.device)
+        ws = self.workspace(n)
+        L.check(self._lib.rtx_shade_hits(blob.data_ptr(), S, si, O.data_ptr(), stride, D.data_ptr(), t.data_ptr(), n,
+                                         self._bounces_arg, res.data_ptr(), _OUT_KIND[self.color_dtype],
+                                         ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream()),
+                "rtx_shade_hits")
+        self._check_status(ws)
+        return res
+
     def _ray_directions(self, camera: Camera) -> torch.Tensor:
         # a camera-only blob: no shapes needed for ray generation
         pos = (float(camera.position.x), float(camera.position.y), float(camera.position.z))

@@ -2,7 +2,8 @@
 
 On this backend a shader is a parameter record: ``HipRenderer`` packs its fields into the scene blob
 (``scene_pack.py``) and the render kernel evaluates ``NumpyShader.create`` (``shader.py:63-112``)
-per hit. The constructor signature, defaults and the four hard-wired physical constants
+per hit; ``HipShader.create`` itself runs that evaluation for a caller-given batch of hits
+(``rtx_shade_hits``). The constructor signature, defaults and the four hard-wired physical constants
 (``specular_ior=1.5``, ``thin_film_weight=0.1``, ``thin_film_thickness=0.3``, ``thin_film_ior=1.4``,
 ``shader.py:51-54``) match the reference, and are writable like there.
 """
@@ -53,6 +54,25 @@ class HipShader(Shader):
         self.thin_film_thickness = 0.3
         self.thin_film_ior = 1.4
 
-    def create(self, *args, **kwargs):
-        raise NotImplementedError(
-            "HipShader is evaluated inside the HipRenderer kernel; use HipRenderer.raytrace_scene")
+    def create(self, shape, scene, ray_origin, normalized_ray_direction, distance, ray_tracer=None):
+        """NumpyShader.create (shader.py:63-112) on the GPU: the colour of the rays (origin,
+        direction) that hit ``shape`` at ``distance`` — shadow, diffuse, dome, specular,
+        iridescence and the reflection recursion (shader.py:143-161), one ``rtx_shade_hits``
+        launch. ``ray_tracer``: the HipRenderer whose bounce cap the reflections follow (the
+        reference re-enters ``ray_tracer.raytrace_scene``); any other value uses an unbounded
+        HipRenderer, as the reference NumpyRenderer recursion is. Returns a HipRGBColor over a
+        [3, n] device tensor."""
+        import copy
+
+        from python_ray_tracer_amd.domain import Scene3D
+
+        from .base import HipRenderer, HipRGBColor
+
+        r = ray_tracer if isinstance(ray_tracer, HipRenderer) else HipRenderer()
+        if getattr(shape, "shader", None) is not self:
+            # the reference shades with this shader's parameters on that shape's geometry
+            proxy = copy.copy(shape)
+            proxy.shader = self
+            shapes = [proxy if s is shape else s for s in scene.shapes]
+            scene, shape = Scene3D(shapes, scene.lights, scene.camera), proxy
+        return HipRGBColor.from_tensor(r.shade_hits(shape, scene, ray_origin, normalized_ray_direction, distance))

@@ -385,3 +385,40 @@ def test_fuzz_scenes_deep_caps(hip, seed):
     assert np.array_equal(O.to_uint8(got, W, H), O.to_uint8(want, W, H))
     s = r.stats()
     assert s["rays"] == st.rays and s["hits"] == st.hits, seed
+
+
+def test_shader_create_matches_reference(hip):
+    """HipShader.create (rtx_shade_hits) == the reference NumpyShader.create called directly
+    (tests/golden/create_kat.*: rays that hit the shape, nearest or not; capped and unbounded),
+    and == the oracle on a larger batch, through the scene's own shader and a foreign one."""
+    z = np.load(GOLDEN / "create_kat.npz")
+    meta = json.loads((GOLDEN / "create_kat.json").read_text())
+    for name, c in meta["cases"].items():
+        scene = scenes.build_scene(c["spec"])
+        shape = scene.shapes[c["shape"]]
+        r = hip.HipRenderer(max_bounces=c["max_bounces"])
+        col = shape.shader.create(shape, scene, hip.HipVector3D(*c["origin"]), hip.HipVector3D(*z[name + "_dirs"]),
+                                  z[name + "_t"], r)
+        assert np.abs(col.data.cpu().numpy() - z[name + "_rgb"]).max() <= ATOL, name
+    # a bigger batch with per-ray origins against the oracle; and another shape's shader
+    spec = scenes.random_spec(16, 3, 80, 45)
+    scene = scenes.build_scene(spec)
+    sc = O.scene_from_spec(spec)
+    d = O.ray_directions(sc.cam, 80, 45)
+    for si, B, foreign in ((16, 3, None), (4, None, None), (16, 2, 7)):
+        t = O.intersect(sc.spheres[si], *sc.cam, *d)
+        hit = t != O.FARAWAY
+        dd = tuple(c[hit] for c in d)
+        r = hip.HipRenderer(max_bounces=B)
+        shader = scene.shapes[si].shader if foreign is None else scene.shapes[foreign].shader
+        got = shader.create(scene.shapes[si], scene, hip.HipVector3D(*sc.cam), hip.HipVector3D(*dd), t[hit], r)
+        osc = sc
+        if foreign is not None:
+            ospec = json.loads(json.dumps(spec))
+            ospec["spheres"][si]["shader"] = spec["spheres"][foreign]["shader"]
+            osc = O.scene_from_spec(ospec)
+        want = np.stack(O.create(osc, si, sc.cam, dd, t[hit], B))
+        assert np.abs(got.data.cpu().numpy() - want).max() <= ATOL, (si, B, foreign)
+    with pytest.raises(ValueError):
+        scene.shapes[0].shader.create(hip.HipSphere(hip.HipVector3D(0, 0, 0), 1.0, None), scene,
+                                      hip.HipVector3D(*sc.cam), hip.HipVector3D(*dd), t[hit], r)
