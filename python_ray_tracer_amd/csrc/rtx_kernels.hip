@@ -72,6 +72,10 @@ constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD oth
 constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
                                      // 8-level instantiation spills, 3 defers too many pixels)
 constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k_render_fast<cap>
+// shading-only terms (the view vector and the specular's internal divisions and square roots, none
+// of which decides a hit, a shadow, a checker cell or a reflected ray) by short Newton sequences
+// without range checks instead of the correctly rounded cores: within ~1 ulp (tools/approx_probe)
+constexpr bool kApproxShading = false;
 // ---- derived ----
 constexpr int kWaveH = 64 / kWaveW;
 static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
@@ -729,11 +733,44 @@ __device__ __forceinline__ double sin_ref(double x) {
   return sin(x);
 }
 
+// Shading-only arithmetic (kApproxShading): operands are positive, normal and far from the
+// overflow range by construction (denominators >= 1e-8, square-root arguments in [0, 2]).
+// rcp: the hardware estimate (~2^-24) and two Newton steps, correctly rounded on 4 M random
+// operands (tools/approx_probe); a * rcp(b) is then within ~1 ulp of a / b.
+__device__ __forceinline__ double div_shade(double a, double b) {
+  if constexpr (!kApproxShading) return div_cr(a, b);
+  double r = __builtin_amdgcn_rcp(b);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  return a * r;
+}
+// sqrt: the library core without its second correction (correctly rounded on the same sample);
+// 0 stays 0 (rsq(0) = inf)
+__device__ __forceinline__ double sqrt_shade(double x) {
+  if constexpr (!kApproxShading) return sqrt_cr(x);
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  const double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return x == 0.0 ? 0.0 : g;
+}
+// 1 / where(|v| == 0, 1, |v|) for d = |v|^2: rsq and two Newton steps (~1 ulp)
+__device__ __forceinline__ double inv_mag_shade(double d) {
+  if constexpr (!kApproxShading) return inv_mag(d);
+  double y = __builtin_amdgcn_rsq(d);
+  y = __builtin_fma(y * 0.5, __builtin_fma(-d * y, y, 1.0), y);
+  y = __builtin_fma(y * 0.5, __builtin_fma(-d * y, y, 1.0), y);
+  return d == 0.0 ? 1.0 : y;
+}
+
 __device__ __forceinline__ double pow5(double x) {
   const double x2 = x * x;
   return (x2 * x2) * x;
 }
-__device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt_cr(x); }
+__device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt_shade(x); }
 
 // The inputs of one shaded hit's colour terms (everything else comes from the material record).
 struct Hit {
@@ -758,7 +795,12 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   double Vx = vx, Vy = vy, Vz = vz;
   norm3_unit(Vx, Vy, Vz);  // :279 (likewise)
   double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
-  norm3(Hx, Hy, Hz);  // :280
+  {  // :280
+    const double rh = inv_mag_shade(dot3(Hx, Hy, Hz, Hx, Hy, Hz));
+    Hx = Hx * rh;
+    Hy = Hy * rh;
+    Hz = Hz * rh;
+  }
   const double NdotV = clip01(dot3(nx, ny, nz, Vx, Vy, Vz));  // :283
   const double NdotH = clip01(dot3(nx, ny, nz, Hx, Hy, Hz));  // :284
   const double VdotH = clip01(dot3(Vx, Vy, Vz, Hx, Hy, Hz));  // :285
@@ -766,12 +808,12 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
   const double a2 = mh[RTX_M_A2];
   const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
-  const double D = div_cr(a2, RTX_PI * ((denom * denom) + 1e-8));  // :296
+  const double D = div_shade(a2, RTX_PI * ((denom * denom) + 1e-8));  // :296
   const double oma2 = mh[RTX_M_1MA2];
-  const double G1L = div_cr(2.0 * NdotL, (NdotL + sqrt_cr(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
-  const double G1V = div_cr(2.0 * NdotV, (NdotV + sqrt_cr(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
+  const double G1L = div_shade(2.0 * NdotL, (NdotL + sqrt_shade(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
+  const double G1V = div_shade(2.0 * NdotV, (NdotV + sqrt_shade(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
   const double G = G1L * G1V;  // :303
-  const double spec_base = div_cr((F * D) * G, (4.0 * NdotV) + 1e-8);  // :306
+  const double spec_base = div_shade((F * D) * G, (4.0 * NdotV) + 1e-8);  // :306
   const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
   const double sf = spec_base + g * glint;  // :315
   return (NdotV <= 0.0) ? 0.0 : sf;  // :318
@@ -905,7 +947,12 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   double spec = 0.0, va = 0.0;
   if (weighted || need_irid) {
     double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
-    norm3(vx, vy, vz);  // :76 (towards the camera on every level)
+    {  // :76 (towards the camera on every level); V only feeds the specular and the iridescence
+      const double rv = inv_mag_shade(dot3(vx, vy, vz, vx, vy, vz));
+      vx = vx * rv;
+      vy = vy * rv;
+      vz = vz * rv;
+    }
     if (weighted) spec = specular(mh, g, nx, ny, nz, lx, ly, lz, vx, vy, vz);
     if (need_irid) va = clip01(dot3(nx, ny, nz, vx, vy, vz));  // :201
   }
