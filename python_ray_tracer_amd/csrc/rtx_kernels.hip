@@ -73,9 +73,11 @@ constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain
                                      // 8-level instantiation spills, 3 defers too many pixels)
 constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k_render_fast<cap>
 // shading-only terms (the view vector and the specular's internal divisions and square roots, none
-// of which decides a hit, a shadow, a checker cell or a reflected ray) by short Newton sequences
-// without range checks instead of the correctly rounded cores: within ~1 ulp (tools/approx_probe)
-constexpr bool kApproxShading = false;
+// of which decides a hit, a shadow, a checker cell or a reflected ray): 0 = the wave-uniform
+// range-checked correctly rounded paths; 1 = the correctly rounded cores without range checks
+// (their operands are in range by construction); 2 = shorter Newton sequences (~1 ulp,
+// tools/approx_probe), which moved C2/C4 colour by up to 1.4e-12 (not adopted)
+constexpr int kShadeMath = 0;
 // ---- derived ----
 constexpr int kWaveH = 64 / kWaveW;
 static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
@@ -733,12 +735,16 @@ __device__ __forceinline__ double sin_ref(double x) {
   return sin(x);
 }
 
-// Shading-only arithmetic (kApproxShading): operands are positive, normal and far from the
-// overflow range by construction (denominators >= 1e-8, square-root arguments in [0, 2]).
+// Shading-only arithmetic (kShadeMath): operands are non-negative and far from the overflow range
+// by construction (denominators >= 1e-8, square-root arguments in [0, 2], |V|^2 and |H|^2 the
+// squared lengths of finite vectors; a zero argument is selected around the core). The cores are
+// bit-identical to the range-checked paths for operands above ~2^-900; below, only terms that are
+// themselves below ~1e-250 can differ.
 // rcp: the hardware estimate (~2^-24) and two Newton steps, correctly rounded on 4 M random
 // operands (tools/approx_probe); a * rcp(b) is then within ~1 ulp of a / b.
 __device__ __forceinline__ double div_shade(double a, double b) {
-  if constexpr (!kApproxShading) return div_cr(a, b);
+  if constexpr (kShadeMath == 0) return div_cr(a, b);
+  if constexpr (kShadeMath == 1) return div_core(a, b);
   double r = __builtin_amdgcn_rcp(b);
   r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
   r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
@@ -747,7 +753,8 @@ __device__ __forceinline__ double div_shade(double a, double b) {
 // sqrt: the library core without its second correction (correctly rounded on the same sample);
 // 0 stays 0 (rsq(0) = inf)
 __device__ __forceinline__ double sqrt_shade(double x) {
-  if constexpr (!kApproxShading) return sqrt_cr(x);
+  if constexpr (kShadeMath == 0) return sqrt_cr(x);
+  if constexpr (kShadeMath == 1) return x == 0.0 ? 0.0 : sqrt_core(x);
   const double y = __builtin_amdgcn_rsq(x);
   double g = x * y, h = y * 0.5;
   const double r = __builtin_fma(-h, g, 0.5);
@@ -759,7 +766,8 @@ __device__ __forceinline__ double sqrt_shade(double x) {
 }
 // 1 / where(|v| == 0, 1, |v|) for d = |v|^2: rsq and two Newton steps (~1 ulp)
 __device__ __forceinline__ double inv_mag_shade(double d) {
-  if constexpr (!kApproxShading) return inv_mag(d);
+  if constexpr (kShadeMath == 0) return inv_mag(d);
+  if constexpr (kShadeMath == 1) return d == 0.0 ? 1.0 : div_core(1.0, sqrt_core(d));
   double y = __builtin_amdgcn_rsq(d);
   y = __builtin_fma(y * 0.5, __builtin_fma(-d * y, y, 1.0), y);
   y = __builtin_fma(y * 0.5, __builtin_fma(-d * y, y, 1.0), y);
