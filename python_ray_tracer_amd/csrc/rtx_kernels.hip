@@ -77,7 +77,7 @@ constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k
 // range-checked correctly rounded paths; 1 = the correctly rounded cores without range checks
 // (their operands are in range by construction); 2 = shorter Newton sequences (~1 ulp,
 // tools/approx_probe), which moved C2/C4 colour by up to 1.4e-12 (not adopted)
-constexpr int kShadeMath = 0;
+constexpr int kShadeMath = 1;
 // ---- derived ----
 constexpr int kWaveH = 64 / kWaveW;
 static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
