@@ -72,12 +72,16 @@ constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD oth
 constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
                                      // 8-level instantiation spills, 3 defers too many pixels)
 constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k_render_fast<cap>
-// shading-only terms (the view vector and the specular's internal divisions and square roots, none
-// of which decides a hit, a shadow, a checker cell or a reflected ray): 0 = the wave-uniform
-// range-checked correctly rounded paths; 1 = the correctly rounded cores without range checks
-// (their operands are in range by construction); 2 = shorter Newton sequences (~1 ulp,
-// tools/approx_probe), which moved C2/C4 colour by up to 1.4e-12 (not adopted)
-constexpr int kShadeMath = 1;
+// shading-only terms (the view vector, the half vector and the specular's internal divisions and
+// square roots; none of them decides a hit, a shadow, a checker cell or a reflected ray):
+//   0 = the wave-uniform range-checked correctly rounded paths;
+//   1 = the correctly rounded cores without range checks (operands in range by construction);
+//   3 = the specular's divisions and square roots by shorter Newton sequences (within ~1 ulp,
+//       tools/approx_probe), V and H normalised by the correctly rounded cores (A/B on identical
+//       parity: C2 -6.4%, C2main -8.5%, C5 -2.9%, C3 -2.8% against 1);
+//   2 / 4 = also V and H (2) or H (4) by rsq + Newton: N.V near grazing amplifies their rounding,
+//       C4 and 1080p colour moved by 1.4e-12 (over the 1e-12 bar), not adopted.
+constexpr int kShadeMath = 3;
 // ---- derived ----
 constexpr int kWaveH = 64 / kWaveW;
 static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
@@ -744,7 +748,7 @@ __device__ __forceinline__ double sin_ref(double x) {
 // operands (tools/approx_probe); a * rcp(b) is then within ~1 ulp of a / b.
 __device__ __forceinline__ double div_shade(double a, double b) {
   if constexpr (kShadeMath == 0) return div_cr(a, b);
-  if constexpr (kShadeMath == 1) return div_core(a, b);
+  if constexpr (kShadeMath == 1) return div_core(a, b);  // (2, 3, 4: the Newton sequence below)
   double r = __builtin_amdgcn_rcp(b);
   r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
   r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
@@ -767,11 +771,18 @@ __device__ __forceinline__ double sqrt_shade(double x) {
 // 1 / where(|v| == 0, 1, |v|) for d = |v|^2: rsq and two Newton steps (~1 ulp)
 __device__ __forceinline__ double inv_mag_shade(double d) {
   if constexpr (kShadeMath == 0) return inv_mag(d);
-  if constexpr (kShadeMath == 1) return d == 0.0 ? 1.0 : div_core(1.0, sqrt_core(d));
+  if constexpr (kShadeMath == 1 || kShadeMath == 3) return d == 0.0 ? 1.0 : div_core(1.0, sqrt_core(d));
   double y = __builtin_amdgcn_rsq(d);
   y = __builtin_fma(y * 0.5, __builtin_fma(-d * y, y, 1.0), y);
   y = __builtin_fma(y * 0.5, __builtin_fma(-d * y, y, 1.0), y);
   return d == 0.0 ? 1.0 : y;
+}
+
+// the view vector: N.V near grazing amplifies its rounding (4 N.V + 1e-8 and G1(N.V) divide by
+// it), so variants 3 and 4 keep its normalisation correctly rounded
+__device__ __forceinline__ double inv_mag_shade_v(double d) {
+  if constexpr (kShadeMath == 3 || kShadeMath == 4) return d == 0.0 ? 1.0 : div_core(1.0, sqrt_core(d));
+  return inv_mag_shade(d);
 }
 
 __device__ __forceinline__ double pow5(double x) {
@@ -804,7 +815,8 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   norm3_unit(Vx, Vy, Vz);  // :279 (likewise)
   double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
   {  // :280
-    const double rh = inv_mag_shade(dot3(Hx, Hy, Hz, Hx, Hy, Hz));
+    const double dh = dot3(Hx, Hy, Hz, Hx, Hy, Hz);
+    const double rh = kShadeMath == 4 ? inv_mag_shade(dh) : inv_mag_shade_v(dh);
     Hx = Hx * rh;
     Hy = Hy * rh;
     Hz = Hz * rh;
@@ -956,7 +968,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   if (weighted || need_irid) {
     double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
     {  // :76 (towards the camera on every level); V only feeds the specular and the iridescence
-      const double rv = inv_mag_shade(dot3(vx, vy, vz, vx, vy, vz));
+      const double rv = inv_mag_shade_v(dot3(vx, vy, vz, vx, vy, vz));
       vx = vx * rv;
       vy = vy * rv;
       vz = vz * rv;
