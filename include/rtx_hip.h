@@ -117,8 +117,9 @@ enum {
 enum {
   RTX_M_G = 0,       /* specular_gain                                      */
   RTX_M_DG = 1,      /* diffuse_gain                                       */
-  RTX_M_TEX = 2,     /* 0 = Texture (constant colour), 1 = TextureChecker  */
-  RTX_M_TR = 3, RTX_M_TG = 4, RTX_M_TB = 5, /* Texture colour            */
+  RTX_M_TEX = 2,     /* RTX_TEX_CONST / _CHECKER / _IMAGE                  */
+  RTX_M_TR = 3, RTX_M_TG = 4, RTX_M_TB = 5, /* Texture colour; IMAGE: texel table word offset in
+                                               the blob, width, height (texels: float64 RGB, row-major) */
   RTX_M_A2 = 6,      /* alpha**2, alpha = specular_roughness**2 (:294-296) */
   RTX_M_A2M1 = 7,    /* alpha**2 - 1                                       */
   RTX_M_1MA2 = 8,    /* 1 - alpha**2                                       */
@@ -134,6 +135,12 @@ enum {
   RTX_M_IOR = 18,
   RTX_M_TFIOR = 19
 };
+
+/* texture kinds (RTX_M_TEX) */
+#define RTX_TEX_CONST 0.0   /* Texture: constant colour (shader.py:13-19)                         */
+#define RTX_TEX_CHECKER 1.0 /* TextureChecker (shader.py:22-32)                                  */
+#define RTX_TEX_IMAGE 2.0   /* ImageTexture: per-point texel of NumpyTexturedSphere's mapping (shape.py:66-79) */
+#define RTX_MAX_TEXELS (1 << 20) /* per image texture */
 
 /* output kinds */
 enum {

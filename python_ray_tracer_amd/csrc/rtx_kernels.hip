@@ -791,6 +791,34 @@ __device__ __forceinline__ double pow5(double x) {
 }
 __device__ __forceinline__ double pow25(double x) { return (x * x) * sqrt_shade(x); }
 
+// A level's key: the hit sphere (RTX_MAX_SPHERES <= 2^kKeyShift) and its texture key above it.
+constexpr int kKeyShift = 11;
+__device__ __forceinline__ int level_key(int hit, int tk) { return hit | (tk << kKeyShift); }
+__device__ __forceinline__ int key_hit(int key) { return key & ((1 << kKeyShift) - 1); }
+__device__ __forceinline__ int key_tex(int key) { return (int)((unsigned)key >> kKeyShift); }
+static_assert(RTX_MAX_SPHERES <= (1 << kKeyShift) && RTX_MAX_TEXELS <= (1 << (31 - kKeyShift)), "level key");
+
+// Image texture (HipTexturedSphere / ImageTexture): the texel of hit point P on sphere (centre C)
+// at the spherical coordinates of NumpyTexturedSphere.diffusecolor (shape.py:66-79): n = (P - C)
+// normalised, u = 0.5 + atan2(n.z, n.x) / (2 pi), v = 0.5 - asin(n.y) / pi, each mod 1, texel
+// (int(v (h-1)), int(u (w-1))). atan2/asin are ROCm's (not correctly rounded, like NumPy's), so
+// a point within an ulp of a texel edge may take the neighbour texel: parity unpinned (the reference
+// class cannot render).
+template <typename T, typename G>
+__device__ __forceinline__ int image_texel(const T* mh, const G* gh, double px, double py, double pz) {
+  double nx = px - gh[RTX_G_CX], ny = py - gh[RTX_G_CY], nz = pz - gh[RTX_G_CZ];
+  norm3(nx, ny, nz);
+  double u = 0.5 + atan2(nz, nx) / (2.0 * RTX_PI);
+  double v = 0.5 - asin(ny) / RTX_PI;
+  u = u - floor(u);  // % 1 (Python / NumPy remainder: non-negative)
+  v = v - floor(v);
+  if (!(u >= 0.0 && u < 1.0)) u = 0.0;  // NaN (a degenerate point): texel 0
+  if (!(v >= 0.0 && v < 1.0)) v = 0.0;
+  const int w = (int)mh[RTX_M_TG], h = (int)mh[RTX_M_TB];
+  const int i = (int)(u * (double)(w - 1)), j = (int)(v * (double)(h - 1));
+  return j * w + i;
+}
+
 // The inputs of one shaded hit's colour terms (everything else comes from the material record).
 struct Hit {
   double dli;    // max(N.L, 0)                                shader.py:138
@@ -799,7 +827,7 @@ struct Hit {
   double va;     // clip(N.V, 0, 1) (iridescence input)         shader.py:201
   double g;      // specular_gain
   int h;         // hit sphere
-  bool chk;      // checker cell                                 shader.py:30
+  int tk;        // texture key: the checker cell (shader.py:30) or the image texel (shape.py:66-79)
   bool lit;      //                                              shader.py:79-84
   double qx, qy, qz;  // nudged hit point = reflected ray origin  shader.py:77
   double nx, ny, nz;  // normal
@@ -844,13 +872,19 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
 //   ((((0.004 + diffuse) + dome) + (spec + R*0.5)*g*lit) + irid)
 // `weighted` = lit && g != 0; otherwise the specular/reflection term is x*0 == 0 (R is finite).
 template <typename M>
-__device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double dli, double di, bool chk, bool lit,
+__device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double dli, double di, int tk, bool lit,
                                           bool weighted, double spec, double va, double Rr, double Rg, double Rb,
                                           double& cr, double& cg, double& cb) {
   const double litf = lit ? 1.0 : 0.0;
   double tr, tg, tb;
-  if (mh[RTX_M_TEX] != 0.0) {  // TextureChecker.get_color (:29-32): white * checker
-    tr = tg = tb = chk ? 1.0 : 0.0;
+  const double tex = mh[RTX_M_TEX];
+  if (tex == RTX_TEX_CHECKER) {  // TextureChecker.get_color (:29-32): white * checker
+    tr = tg = tb = tk ? 1.0 : 0.0;
+  } else if (tex == RTX_TEX_IMAGE) {  // the texel shade() picked (texel table in the blob)
+    const cdouble* t = sc + ((int64_t)mh[RTX_M_TR] + 3 * (int64_t)tk);
+    tr = t[0];
+    tg = t[1];
+    tb = t[2];
   } else {  // Texture.get_color (:17-19)
     tr = mh[RTX_M_TR];
     tg = mh[RTX_M_TG];
@@ -982,7 +1016,9 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   s.va = va;
   s.g = g;
   s.h = h;
-  s.chk = (mh[RTX_M_TEX] != 0.0) && (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0));  // :30
+  const double tex = mh[RTX_M_TEX];
+  s.tk = tex == RTX_TEX_CHECKER ? (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0))  // :30
+         : tex == RTX_TEX_IMAGE ? image_texel(mh, gh, px, py, pz) : 0;
   s.lit = lit;
   s.qx = qx; s.qy = qy; s.qz = qz;
   s.nx = nx; s.ny = ny; s.nz = nz;
@@ -1237,7 +1273,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         rec[3] = rx; rec[4] = ry; rec[5] = rz;
         for (int w = 0; w < kRecLevelWords * kb; ++w) rec[6 + w] = rin[6 + w];  // levels 0..kb-1
         double* lv = rec + 6 + kRecLevelWords * (kb + B);
-        lv[0] = s.dli; lv[1] = s.di; lv[2] = s.spec; lv[3] = s.va; lv[4] = (double)(hit | (s.chk ? 0x10000 : 0));
+        lv[0] = s.dli; lv[1] = s.di; lv[2] = s.spec; lv[3] = s.va; lv[4] = (double)level_key(hit, s.tk);
         if constexpr (LV) {  // LDS slot d = level kb + d (a DEEP kernel keeps all B levels there)
           static_assert(!LV || !DEEP || NL == B, "DEEP level slots");
           for (int d = 0; d < NL; ++d) {
@@ -1259,7 +1295,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (!weighted || k >= B || at_cap) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
       const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
-      hit_color(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.chk, s.lit, weighted, s.spec,
+      hit_color(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
                 s.va, 0.0, 0.0, 0.0, cr, cg, cb);
       break;
     }
@@ -1268,7 +1304,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       if (NL == B || k < NL) {  // k: wave-uniform, == depth of every active lane
         double* const l = lvd + (depth * 4) * kFastBlock + lt;
         l[0] = s.dli; l[kFastBlock] = s.di; l[2 * kFastBlock] = s.spec; l[3 * kFastBlock] = s.va;
-        lvk[depth * kFastBlock + lt] = hit | (s.chk ? 0x10000 : 0);
+        lvk[depth * kFastBlock + lt] = level_key(hit, s.tk);
       } else {  // levels beyond the LDS slots: a register shift (slot 0 = the most recent)
 #pragma unroll
         for (int j = NR - 1; j > 0; --j) {
@@ -1276,7 +1312,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
           sKey[j] = sKey[j - 1];
         }
         sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
-        sKey[0] = hit | (s.chk ? 0x10000 : 0);
+        sKey[0] = level_key(hit, s.tk);
       }
     } else {
 #pragma unroll
@@ -1285,7 +1321,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         sKey[j] = sKey[j - 1];
       }
       sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
-      sKey[0] = hit | (s.chk ? 0x10000 : 0);
+      sKey[0] = level_key(hit, s.tk);
     }
     ++depth;
     reflect_dir(dx, dy, dz, s.nx, s.ny, s.nz);
@@ -1324,7 +1360,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if constexpr (NL < B) {
       for (int d = depth - 1; d >= NL; --d) {  // the register levels first (the deepest)
         const int key = sKey[0];
-        hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true,
+        hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], key_tex(key), true, true,
                   sSpec[0], sVa[0], cr, cg, cb, cr, cg, cb);
 #pragma unroll
         for (int j = 0; j < NR - 1; ++j) {
@@ -1336,13 +1372,13 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     for (int d = (depth < NL ? depth : NL) - 1; d >= 0; --d) {
       const double* const l = lvd + (d * 4) * kFastBlock + lt;
       const int key = lvk[d * kFastBlock + lt];
-      hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, l[0], l[kFastBlock], (key >> 16) != 0, true, true,
+      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, l[0], l[kFastBlock], key_tex(key), true, true,
                 l[2 * kFastBlock], l[3 * kFastBlock], cr, cg, cb, cr, cg, cb);
     }
   } else {
     for (int d = 0; d < depth; ++d) {
       const int key = sKey[0];
-      hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], (key >> 16) != 0, true, true, sSpec[0],
+      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], key_tex(key), true, true, sSpec[0],
                 sVa[0], cr, cg, cb, cr, cg, cb);
 #pragma unroll
       for (int j = 0; j < NS - 1; ++j) {
@@ -1355,7 +1391,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     for (int l = kb - 1; l >= 0; --l) {
       const double* lv = rin + 6 + kRecLevelWords * l;
       const int key = (int)lv[4];
-      hit_color(mtab + (key & 0xFFFF) * RTX_MAT_WORDS, sc, lv[0], lv[1], (key >> 16) != 0, true, true, lv[2], lv[3],
+      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, lv[0], lv[1], key_tex(key), true, true, lv[2], lv[3],
                 cr, cg, cb, cr, cg, cb);
     }
   }
@@ -1477,7 +1513,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       S.at(l, F_DLI) = lv[0]; S.at(l, F_DI) = lv[1]; S.at(l, F_SPEC) = lv[2]; S.at(l, F_VA) = lv[3];
       S.at(l, F_KEY) = lv[4];
       S.at(l, F_AR) = 0.0; S.at(l, F_AG) = 0.0; S.at(l, F_AB) = 0.0;
-      S.at(l, F_NEXT) = (double)(((int)lv[4] & 0xFFFF) + 1);
+      S.at(l, F_NEXT) = (double)(key_hit((int)lv[4]) + 1);
       S.at(l, F_LEFT) = 1.0;
     }
     d = L + 1;
@@ -1543,9 +1579,9 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       }
       --d;  // fold into the parent's pending hit (shader.py:106-110), then add (base.py:119)
       const int key = (int)S.at(d, F_KEY);
-      const int ph = key & 0xFFFF;
+      const int ph = key_hit(key);
       double xr, xg, xb;
-      hit_color(mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI), (key >> 16) != 0, true, true,
+      hit_color(mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI), key_tex(key), true, true,
                 S.at(d, F_SPEC), S.at(d, F_VA), rr, rg, rb, xr, xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
@@ -1566,7 +1602,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     }
     if (!descend) {
       double xr, xg, xb;
-      hit_color(mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.chk, s.lit, weighted, s.spec, s.va, 0.0, 0.0, 0.0, xr,
+      hit_color(mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec, s.va, 0.0, 0.0, 0.0, xr,
                 xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
@@ -1576,7 +1612,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       continue;
     }
     S.at(d, F_DLI) = s.dli; S.at(d, F_DI) = s.di; S.at(d, F_SPEC) = s.spec; S.at(d, F_VA) = s.va;
-    S.at(d, F_KEY) = (double)(h | (s.chk ? 0x10000 : 0));
+    S.at(d, F_KEY) = (double)level_key(h, s.tk);
     double rx = dx, ry = dy, rz = dz;
     reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
     ++d;

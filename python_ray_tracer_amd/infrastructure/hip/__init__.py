@@ -3,9 +3,9 @@
 Reference module -> this module:
   numpy/base.py   NumpyVector3D, NumpyVectorArray3D, NumpyRGBColor, NumpyRenderer, FARAWAY
                -> hip/base.py  HipVector3D, HipVectorArray3D, HipRGBColor, HipRenderer, FARAWAY
-  numpy/shape.py  NumpySphere            -> hip/shape.py  HipSphere
+  numpy/shape.py  NumpySphere, NumpyTexturedSphere -> hip/shape.py  HipSphere, HipTexturedSphere
   numpy/shader.py Texture, TextureChecker, NumpyShader
-               -> hip/shader.py Texture, TextureChecker, HipShader
+               -> hip/shader.py Texture, TextureChecker, ImageTexture, HipShader
 """
 
 from .base import (
@@ -16,8 +16,8 @@ from .base import (
     HipVector3D,
     HipVectorArray3D,
 )
-from .shader import HipShader, Texture, TextureChecker
-from .shape import HipSphere
+from .shader import HipShader, ImageTexture, Texture, TextureChecker
+from .shape import HipSphere, HipTexturedSphere
 
 __all__ = [
     "FARAWAY",
@@ -26,6 +26,8 @@ __all__ = [
     "HipRGBColor",
     "HipShader",
     "HipSphere",
+    "HipTexturedSphere",
+    "ImageTexture",
     "HipVector3D",
     "HipVectorArray3D",
     "Texture",

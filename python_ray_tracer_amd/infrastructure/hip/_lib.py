@@ -30,6 +30,9 @@ MAX_SPHERES = 1024
 MAGIC = 5527384.0
 UNBOUNDED = -1
 
+TEX_CONST, TEX_CHECKER, TEX_IMAGE = 0.0, 1.0, 2.0
+MAX_TEXELS = 1 << 20
+
 OUT_F32_SOA = 0
 OUT_F64_SOA = 1
 OUT_U8_HWC = 2

@@ -63,7 +63,10 @@ def _shape_fields(shape):
     sh = shape.shader
     tex = sh.diffuse_color
     if type(tex).__name__ == "TextureChecker":
-        tex_fields = (1.0, 1.0, 1.0, 1.0)
+        tex_fields = (L.TEX_CHECKER, 1.0, 1.0, 1.0)
+    elif hasattr(tex, "texels") and hasattr(tex, "digest"):  # ImageTexture
+        tex_fields = (L.TEX_IMAGE, _Texels(tex.texels, tex.digest), float(tex.texels.shape[1]),
+                      float(tex.texels.shape[0]))
     elif hasattr(tex, "color"):
         tex_fields = (0.0,) + _xyz(tex.color)
     else:
@@ -72,6 +75,22 @@ def _shape_fields(shape):
     return (_xyz(pos), shape.radius, tex_fields, sh.specular_gain, sh.diffuse_gain, sh.specular_roughness,
             sh.specular_ior, sh.iridescence_gain, sh.thin_film_weight, sh.thin_film_thickness, sh.thin_film_ior,
             sh.reflection_gain)
+
+
+class _Texels:
+    """An image texture's texels inside a hashable scene key (hashed by content digest)."""
+
+    __slots__ = ("texels", "digest")
+
+    def __init__(self, texels, digest) -> None:
+        self.texels = texels
+        self.digest = digest
+
+    def __hash__(self) -> int:
+        return hash(self.digest)
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, _Texels) and other.digest == self.digest
 
 
 def scene_key(scene) -> tuple:
@@ -139,7 +158,10 @@ def _pack_static(static: tuple) -> np.ndarray:
         m = [0.0] * L.MAT_WORDS
         m[L.M_G] = g
         m[L.M_DG] = dg
-        m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = tex
+        if tex[0] == L.TEX_IMAGE:  # the texel table's offset is set below, once the blob is laid out
+            m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = L.TEX_IMAGE, 0.0, tex[2], tex[3]
+        else:
+            m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = tex
         # _calculate_physical_specular constants (shader.py:290-301), same Python expressions
         alpha = rough**2
         F0 = ((ior - 1) / (ior + 1)) ** 2
@@ -165,6 +187,21 @@ def _pack_static(static: tuple) -> np.ndarray:
     blob[L.HDR_WORDS + S * L.GEOM_WORDS:] = np.asarray(mat_rows, dtype=np.float64).ravel()
     if S >= BVH_MIN_SPHERES:
         blob = _append_culling_tree(blob, geo.copy(), S)
+    # image textures: one float64 RGB texel table per distinct image, after everything else; the
+    # material's RTX_M_TR word holds its word offset
+    textures, offsets, size = [], {}, blob.size
+    for s_idx, sp in enumerate(spheres):
+        tex = sp[2]
+        if tex[0] != L.TEX_IMAGE:
+            continue
+        ref = tex[1]
+        if ref.digest not in offsets:
+            offsets[ref.digest] = size
+            size += ref.texels.size
+            textures.append(ref.texels)
+        blob[L.HDR_WORDS + S * L.GEOM_WORDS + s_idx * L.MAT_WORDS + L.M_TR] = offsets[ref.digest]
+    if textures:
+        blob = np.concatenate([blob] + [t.ravel() for t in textures])
     blob.setflags(write=False)
     return blob
 

@@ -38,6 +38,41 @@ class TextureChecker(Texture):
         return HipRGBColor(1 * checker, 1 * checker, 1 * checker)
 
 
+class ImageTexture(Texture):
+    """An image as a diffuse texture, looked up per hit point at the spherical coordinates of the
+    reference's ``NumpyTexturedSphere.diffusecolor`` (shape.py:66-79) about the hit sphere's
+    centre. ``image``: a path (loaded like shape.py:64-65, ``np.asarray(Image.open(p).convert("RGB"))
+    / 255.0``), an (H, W, 3) uint8 array (divided by 255.0 the same way) or an (H, W, 3) float array
+    of texel colours. The reference class averages the texels of all points handed to one call into a
+    single colour (shape.py:81-90), which makes it depend on how rays are batched, and cannot render
+    at all (its shader is a colour, shape.py:64); this is the per-point lookup it evidently intends.
+    At most 2^20 texels."""
+
+    def __init__(self, image) -> None:
+        import hashlib
+
+        import numpy as np
+
+        if isinstance(image, (str, bytes)) or hasattr(image, "__fspath__"):
+            from PIL import Image
+
+            arr = np.asarray(Image.open(image).convert("RGB")) / 255.0  # shape.py:64-65
+        else:
+            arr = np.asarray(image)
+            arr = arr / 255.0 if arr.dtype == np.uint8 else arr.astype(np.float64)
+        if arr.ndim != 3 or arr.shape[2] < 3 or arr.shape[0] < 1 or arr.shape[1] < 1:
+            raise ValueError(f"image texture: need an (H, W, 3) image, got shape {arr.shape}")
+        self.texels = np.ascontiguousarray(arr[:, :, :3], dtype=np.float64)
+        if self.texels.shape[0] * self.texels.shape[1] > (1 << 20):
+            raise ValueError("image texture: at most 2^20 texels")
+        self.digest = hashlib.blake2b(self.texels.tobytes() + repr(self.texels.shape).encode(),
+                                      digest_size=16).hexdigest()
+        super().__init__(HipRGBColor(1, 1, 1))
+
+    def get_color(self, intersection_point):
+        raise NotImplementedError("ImageTexture is evaluated per hit inside the HipRenderer kernel")
+
+
 class HipShader(Shader):
     """NumpyShader parameters (shader.py:36-54)."""
 

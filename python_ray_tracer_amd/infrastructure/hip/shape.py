@@ -47,4 +47,23 @@ class HipSphere(Shape):
         return self.shader.diffuse_color.get_color(intersection_point)
 
 
-__all__ = ["HipSphere", "HipVector3D"]
+class HipTexturedSphere(HipSphere):
+    """Reference ``NumpyTexturedSphere(center, radius, texture_path)`` (shape.py:57-90): a sphere
+    whose diffuse colour is an image mapped by spherical coordinates. The reference passes an RGB
+    colour as its shader and cannot render (base.py:110); here the image is an ``ImageTexture`` of
+    the sphere's shader: by default ``HipShader(0.0, 0.0, 0.5, 0.0, 1.0, ImageTexture(path))`` (pure
+    diffuse), or ``shader`` with its ``diffuse_color`` replaced by the image."""
+
+    def __init__(self, center, radius: float, texture_path, shader=None) -> None:
+        from .shader import HipShader, ImageTexture
+
+        tex = ImageTexture(texture_path)
+        if shader is None:
+            shader = HipShader(0.0, 0.0, 0.5, 0.0, 1.0, tex)
+        else:
+            shader.diffuse_color = tex
+        super().__init__(center, radius, shader)
+        self.image = tex
+
+
+__all__ = ["HipSphere", "HipTexturedSphere", "HipVector3D"]

@@ -21,6 +21,7 @@ Spec layout::
                   "shader": {"reflection_gain": .., "specular_gain": .., "specular_roughness": ..,
                              "iridescence_gain": .., "diffuse_gain": ..,
                              "texture": {"kind": "const" | "checker", "color": [r, g, b]}}}],
+                  (or {"kind": "image", "texels": (H, W, 3) float colours} — ImageTexture)
      "lights": [{"kind": "point", "position": [x, y, z]},
                 {"kind": "dome", "intensity": i, "color": [r, g, b]}],
      "camera": {"position": [x, y, z], "width": W, "height": H}}
@@ -160,6 +161,7 @@ def build_scene(spec: dict):
         HipShader,
         HipSphere,
         HipVector3D,
+        ImageTexture,
         Texture,
         TextureChecker,
     )
@@ -168,7 +170,12 @@ def build_scene(spec: dict):
     for s in spec["spheres"]:
         sh = s["shader"]
         tex = sh["texture"]
-        texture = TextureChecker() if tex["kind"] == "checker" else Texture(HipRGBColor(*tex["color"]))
+        if tex["kind"] == "checker":
+            texture = TextureChecker()
+        elif tex["kind"] == "image":
+            texture = ImageTexture(np.asarray(tex["texels"], dtype=np.float64))
+        else:
+            texture = Texture(HipRGBColor(*tex["color"]))
         shader = HipShader(sh["reflection_gain"], sh["specular_gain"], sh["specular_roughness"],
                            sh["iridescence_gain"], sh["diffuse_gain"], texture)
         shapes.append(HipSphere(HipVector3D(*s["center"]), s["radius"], shader))

@@ -422,3 +422,45 @@ def test_shader_create_matches_reference(hip):
     with pytest.raises(ValueError):
         scene.shapes[0].shader.create(hip.HipSphere(hip.HipVector3D(0, 0, 0), 1.0, None), scene,
                                       hip.HipVector3D(*sc.cam), hip.HipVector3D(*dd), t[hit], r)
+
+
+def _textured_spec(W, H):
+    """The README scene plus two image-textured spheres (a mirror-ish one and a diffuse one)."""
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, size=(40, 64, 3)).astype(np.float64) / 255.0
+    spec = scenes.readme_spec(W, H)
+    spec["spheres"].insert(0, {"center": [-0.9, 0.2, 2.0], "radius": 0.6,
+                               "shader": {"reflection_gain": 0.0, "specular_gain": 0.0, "specular_roughness": 0.5,
+                                          "iridescence_gain": 0.0, "diffuse_gain": 1.0,
+                                          "texture": {"kind": "image", "texels": img}}})
+    spec["spheres"].insert(1, {"center": [1.2, 0.0, 1.5], "radius": 0.5,
+                               "shader": {"reflection_gain": 0.5, "specular_gain": 0.7, "specular_roughness": 0.2,
+                                          "iridescence_gain": 0.05, "diffuse_gain": 0.8,
+                                          "texture": {"kind": "image", "texels": img[::-1].copy()}}})
+    return spec
+
+
+@pytest.mark.parametrize("B", [3, None])
+def test_image_textured_spheres(hip, B):
+    """ImageTexture / HipTexturedSphere (the per-point mapping of shape.py:66-79, pinned on the
+    reference's own diffusecolor by tests/golden/texture_kat.json through the oracle): renders
+    against the oracle. ROCm's atan2/asin and NumPy's may pick the neighbour texel for a point
+    within an ulp of a texel edge (parity unpinned at that level): at most 1 pixel in 10^4 may differ,
+    every other pixel within 1e-12. Also through reflections (the mirror-ish sphere) and create()."""
+    spec = _textured_spec(160, 90)
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    bad = (np.abs(got - want) > ATOL).any(axis=0)
+    assert bad.sum() <= max(1, got.shape[1] // 10000), bad.sum()
+    assert r.stats()["rays"] == st.rays
+    # HipTexturedSphere (the reference class's signature) == ImageTexture through HipShader
+    from python_ray_tracer_amd.domain import Scene3D
+
+    scene = scenes.build_scene(spec)
+    img = spec["spheres"][0]["shader"]["texture"]["texels"]
+    ts = hip.HipTexturedSphere(hip.HipVector3D(-0.9, 0.2, 2.0), 0.6, (img * 255).round().astype(np.uint8))
+    scene2 = Scene3D([ts] + list(scene.shapes)[1:], scene.lights, scene.camera)
+    r2 = hip.HipRenderer(max_bounces=B)
+    got2 = r2.render(scene2).data.cpu().numpy()
+    assert np.abs(got2 - got).max() <= ATOL

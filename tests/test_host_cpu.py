@@ -301,3 +301,25 @@ def test_torch_ops_registered_and_checked_on_host():
         torch.ops.rt.quantize_u8(torch.zeros(3, 4))
     with pytest.raises(RuntimeError):
         torch.ops.rt.assemble_rows(torch.zeros(2, 64, dtype=torch.uint8), 4, 4, 1, 2)
+
+
+def test_pack_image_texture():
+    """An ImageTexture packs as RTX_TEX_IMAGE with its float64 texels (uint8 / 255.0, shape.py:65)
+    appended once per distinct image; the material words hold the table offset, width, height."""
+    from python_ray_tracer_amd.domain import Scene3D
+    from python_ray_tracer_amd.infrastructure.hip import HipTexturedSphere, HipVector3D, ImageTexture
+
+    sc = scenes.build_scene(scenes.random_spec(9, 2, 16, 9))  # 10 spheres: the culling tree too
+    img = (np.arange(5 * 7 * 3).reshape(5, 7, 3) * 7 % 256).astype(np.uint8)
+    a = HipTexturedSphere(HipVector3D(0, 0.5, 2), 0.7, img)
+    b = HipTexturedSphere(HipVector3D(1, 0.5, 3), 0.4, img.copy())  # same content: one table
+    blob = scene_pack.pack_scene(Scene3D(list(sc.shapes) + [a, b], sc.lights, sc.camera))
+    S = 12
+    mat = blob[L.HDR_WORDS + S * L.GEOM_WORDS:L.HDR_WORDS + S * (L.GEOM_WORDS + L.MAT_WORDS)].reshape(S, -1)
+    assert mat[10, L.M_TEX] == L.TEX_IMAGE and mat[11, L.M_TEX] == L.TEX_IMAGE
+    assert mat[10, L.M_TR] == mat[11, L.M_TR] and (mat[10, L.M_TG], mat[10, L.M_TB]) == (7, 5)
+    off = int(mat[10, L.M_TR])
+    assert off + 105 == blob.size and np.array_equal(blob[off:].reshape(5, 7, 3), img / 255.0)
+    assert blob[L.H_NNODES] > 0  # the tree sits before the texels
+    with pytest.raises(ValueError):
+        ImageTexture(np.zeros((4, 4)))

@@ -120,3 +120,16 @@ def test_oracle_render_rows_equals_full_frame_rows():
     for P, p in ((3, 1), (5, 4)):
         rows = tiling.tile_rows(37, 4, P, p)
         assert np.array_equal(O.render_rows(sc, rows, 4), full[:, rows].reshape(3, -1))
+
+
+def test_oracle_image_texels_match_reference_textured_sphere():
+    """O.image_texels == the reference NumpyTexturedSphere.diffusecolor (shape.py:66-79) evaluated
+    on single points (tests/golden/make_golden_texture.py): random points, poles, the u seam."""
+    import json
+
+    k = json.loads((GOLDEN / "texture_kat.json").read_text())
+    sp = O.OSphere(*k["center"], k["radius"], 0, 0, 0, 0, 1, False, (1, 1, 1),
+                   image=np.asarray(k["image"], dtype=np.uint8) / 255.0)
+    P = np.asarray(k["points"])
+    got = np.stack(O.image_texels(sp, P[:, 0], P[:, 1], P[:, 2]), 1)
+    assert np.array_equal(got, np.asarray(k["rgb"]))
