@@ -871,7 +871,10 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
 // Colour of one shaded hit given the reflected colour R (shader.py:86-110):
 //   ((((0.004 + diffuse) + dome) + (spec + R*0.5)*g*lit) + irid)
 // `weighted` = lit && g != 0; otherwise the specular/reflection term is x*0 == 0 (R is finite).
-template <typename M>
+// IMG: image textures are handled (the general kernel); k_render_fast defers every pixel that
+// meets an image-textured sphere, so its instantiations compile no texture lookup (A/B: carrying
+// the lookup cost C2 +3.4%, C2main +7%).
+template <bool IMG = false, typename M>
 __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double dli, double di, int tk, bool lit,
                                           bool weighted, double spec, double va, double Rr, double Rg, double Rb,
                                           double& cr, double& cg, double& cb) {
@@ -880,7 +883,7 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   const double tex = mh[RTX_M_TEX];
   if (tex == RTX_TEX_CHECKER) {  // TextureChecker.get_color (:29-32): white * checker
     tr = tg = tb = tk ? 1.0 : 0.0;
-  } else if (tex == RTX_TEX_IMAGE) {  // the texel shade() picked (texel table in the blob)
+  } else if (IMG && tex == RTX_TEX_IMAGE) {  // the texel shade() picked (texel table in the blob)
     const cdouble* t = sc + ((int64_t)mh[RTX_M_TR] + 3 * (int64_t)tk);
     tr = t[0];
     tg = t[1];
@@ -925,7 +928,7 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 // assembly (hit_color) and the reflection recursion (driven by the caller).
 // geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
 // same table (LDS copy or global).
-template <typename T, typename G, typename Wk>
+template <bool IMG = false, typename T, typename G, typename Wk>
 __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* tab, int nsph, int h, double ox,
                                       double oy, double oz, double dx, double dy, double dz, double t, Hit& s,
                                       Wk& wk) {
@@ -1018,7 +1021,8 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   s.h = h;
   const double tex = mh[RTX_M_TEX];
   s.tk = tex == RTX_TEX_CHECKER ? (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0))  // :30
-         : tex == RTX_TEX_IMAGE ? image_texel(mh, gh, px, py, pz) : 0;
+         : tex != RTX_TEX_IMAGE ? 0
+         : IMG ? image_texel(mh, gh, px, py, pz) : -1;  // -1: k_render_fast defers the ray
   s.lit = lit;
   s.qx = qx; s.qy = qy; s.qz = qz;
   s.nx = nx; s.ny = ny; s.nz = nz;
@@ -1246,15 +1250,21 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       if (st) stat_add(st, RTX_S_TIES, 1);
       break;
     }
-    if (st && kb + k < RTX_S_LEVELS) {
-      stat_add(st, RTX_S_HITS + kb + k, 1);
-      stat_wave(st, RTX_S_WSHADE + kb + k);
-    }
     Hit s;
     if constexpr (LDS) {
       shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, wk);
     } else {
       shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, wk);
+    }
+    if (s.tk < 0) {  // an image-textured sphere: so is this one (the texel lookup stays out of here)
+      deferred = true;
+      rays_through = kb + k;
+      hits_through = kb + k - 1;
+      break;
+    }
+    if (st && kb + k < RTX_S_LEVELS) {
+      stat_add(st, RTX_S_HITS + kb + k, 1);
+      stat_wave(st, RTX_S_WSHADE + kb + k);
     }
     const bool weighted = s.lit && s.g != 0.0;
     // the cap itself (absolute level; a continuation pass may run into a cap of 9 or 10)
@@ -1581,7 +1591,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       const int key = (int)S.at(d, F_KEY);
       const int ph = key_hit(key);
       double xr, xg, xb;
-      hit_color(mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI), key_tex(key), true, true,
+      hit_color<true>(mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI), key_tex(key), true, true,
                 S.at(d, F_SPEC), S.at(d, F_VA), rr, rg, rb, xr, xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
@@ -1593,7 +1603,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     if (st && d < RTX_S_LEVELS && d > hits_through) stat_add(st, RTX_S_HITS + d, 1);
     Hit s;
     Work<false> nowk;
-    shade(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, nowk);
+    shade<true>(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, nowk);
     const bool weighted = s.lit && s.g != 0.0;
     bool descend = weighted && (B < 0 || d < B);
     if (descend && d + 1 >= p.stack_levels) {  // deeper than the stack: RecursionError on the host
@@ -1602,7 +1612,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     }
     if (!descend) {
       double xr, xg, xb;
-      hit_color(mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec, s.va, 0.0, 0.0, 0.0, xr,
+      hit_color<true>(mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec, s.va, 0.0, 0.0, 0.0, xr,
                 xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
