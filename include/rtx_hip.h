@@ -82,7 +82,10 @@ enum {
   RTX_H_NNODES = 33, /* bounding-sphere tree nodes, depth-first order                        */
   RTX_H_NALWAYS = 34,/* leading entries of the culled geometry list tested by every ray (huge spheres) */
   RTX_H_NODES = 35,  /* word offset of the node array (RTX_NODE_WORDS each)                 */
-  RTX_H_CGEO = 36    /* word offset of the culled geometry list (S records, RTX_GEOM_WORDS)  */
+  RTX_H_CGEO = 36,   /* word offset of the culled geometry list (S records, RTX_GEOM_WORDS)  */
+  RTX_H_TAME = 37    /* 1: every coordinate (centres, camera) and radius below 2^60 in magnitude, so
+                        the fast kernel may use the half-b sphere test (rtx_kernels.hip SphTest); 0: the
+                        reference expressions everywhere */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 

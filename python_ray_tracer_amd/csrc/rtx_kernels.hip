@@ -360,52 +360,111 @@ __device__ __forceinline__ double isect(const P* g, double ox, double oy, double
 }
 
 // The same test split in two halves so that two spheres' dependency chains interleave (and their
-// scalar loads share one wait): isect_disc computes b and the discriminant, isect_sol the rest.
+// scalar loads share one wait): isect_disc computes the quadratic's coefficients, isect_sol the rest.
+//
+// Half-b form. With h = D.(O - C) the reference's b is 2h exactly, b*b = 4 fl(h*h), 4c is exact,
+// disc = 4 fl(fl(h*h) - c) = 4q, sqrt(disc) = 2 sqrt(q) and its roots (-b -+ sqrt(disc)) / 2 are
+// fl(-h -+ sqrt(q)): bit for bit the same numbers, four multiplications and the range checks
+// fewer. Each step is an exact scaling by a power of two as long as nothing leaves the normal
+// range: h*h must be normal and not overflow, 4c must not overflow. The host marks a scene "tame"
+// (RTX_H_TAME) when every coordinate and radius is below 2^60, so that |O|, |O - C| stay below
+// ~2^140 for every origin a hit can produce (t < FARAWAY ~ 2^130) and |h| < 2^141, |c| < 2^284;
+// the lower end is checked per wave: |h| >= 2^-350 in every active lane. Then q is 0 or at least
+// 2^-753 in magnitude (h*h >= 2^-700; a nonzero q = fl(h*h) - c is either above half of h*h or an
+// exact Sterbenz difference, a multiple of ulp(h*h)/2), so q is inside sqrt_core's exact range,
+// and -h -+ sqrt(q) is 0 or normal. Explicit-ray launches and untamed scenes, and any wave with a
+// lane at |h| < 2^-350 (a ray at right angles to O - C, such as tests/golden/intersect_kat.json's
+// b = 1.6e-162 case), evaluate the reference expressions instead.
+struct SphTest {
+  double h, d;  // h = D.(O - C); d: q (half) or the reference's disc = (2h)^2 - 4c
+  bool skip;    // no hit in this lane: d <= 0, or the sphere lies behind the origin
+  int half;     // wave-uniform (an int: a uniform bool carried across blocks costs VALU copies)
+};
+// h > 0 and c >= 0 (|h| >= 2^-350): q <= fl(h*h) and sqrt(fl(h*h)) == h, so -h + sqrt(q) <= 0
+// tame: the lower bound 2^-350 in a tame launch, NaN otherwise (no |h| passes; a double threshold
+// keeps the uniform flag out of lane-mask copies)
+__device__ __forceinline__ SphTest sph_test(double h, double c, double tame) {
+  SphTest t;
+  t.half = __ballot(!(fabs(h) >= tame)) == 0 ? 1 : 0;
+  t.h = h;
+  if (t.half) {
+    t.d = (h * h) - c;
+    t.skip = !(t.d > 0.0) || (h > 0.0 && c >= 0.0);
+  } else {
+    const double b = 2.0 * h;  // b = 2.0 * D.(O - C), shape.py:33-37
+    t.d = (b * b) - (4.0 * c);
+    t.skip = !(t.d > 0.0) || behind(b, c);
+  }
+  return t;
+}
 template <typename P>
-__device__ __forceinline__ void isect_disc(const P* g, double ox, double oy, double oz, double oo, double dx,
-                                           double dy, double dz, double& b, double& disc, bool& skip) {
+__device__ __forceinline__ SphTest isect_disc(const P* g, double ox, double oy, double oz, double oo, double dx,
+                                              double dy, double dz, double tame) {
   const double cx = g[RTX_G_CX], cy = g[RTX_G_CY], cz = g[RTX_G_CZ];
-  b = 2.0 * dot3(dx, dy, dz, ox - cx, oy - cy, oz - cz);
+  const double h = dot3(dx, dy, dz, ox - cx, oy - cy, oz - cz);
   const double c = ((g[RTX_G_CC] + oo) - 2.0 * dot3(cx, cy, cz, ox, oy, oz)) - g[RTX_G_RR];
-  disc = (b * b) - (4.0 * c);
-  skip = !(disc > 0.0) || behind(b, c);
+  return sph_test(h, c, tame);
 }
 // level-0 camera origin: O - C from uniform values, c precomputed on the host (same expressions)
 template <typename P>
-__device__ __forceinline__ void isect_disc_cam(const P* g, double ox, double oy, double oz, double dx, double dy,
-                                               double dz, double& b, double& disc, bool& skip) {
-  b = 2.0 * dot3(dx, dy, dz, ox - g[RTX_G_CX], oy - g[RTX_G_CY], oz - g[RTX_G_CZ]);
-  const double c = g[RTX_G_C0];
-  disc = (b * b) - (4.0 * c);
-  skip = !(disc > 0.0) || behind(b, c);
+__device__ __forceinline__ SphTest isect_disc_cam(const P* g, double ox, double oy, double oz, double dx, double dy,
+                                                  double dz, double tame) {
+  const double h = dot3(dx, dy, dz, ox - g[RTX_G_CX], oy - g[RTX_G_CY], oz - g[RTX_G_CZ]);
+  return sph_test(h, g[RTX_G_C0], tame);
 }
 // The rest of the test, as a root and a validity flag instead of the FARAWAY sentinel (no f64
 // selects of a non-inline constant): valid <=> the reference returns the root, not FARAWAY. With
-// s0 <= s1 (rounding is monotone), (s0 > 0 ? s0 : s1) > 0 <=> s1 > 0. Lanes with disc <= 0 take
-// sqrt(|disc|), a discarded dummy that keeps them on sqrt_cr's fast path.
-__device__ __forceinline__ double isect_sol(double b, double disc, bool& valid) {
-  const double sq = sqrt_cr(fabs(disc));
+// s0 <= s1 (rounding is monotone), (s0 > 0 ? s0 : s1) > 0 <=> s1 > 0. Lanes without a root take
+// the square root of |disc|, a discarded dummy.
+__device__ __forceinline__ double isect_sol(const SphTest& t, bool& valid) {
+  if (t.half) {
+    // s1 = fl(-h + sq) > 0 <=> sq > h and s0 > 0 <=> -h > sq (a sum of two doubles rounds to 0 only
+    // when it is 0); the root is -h + (s0 > 0 ? -sq : sq), -sq by flipping the high word's sign.
+    // (skip covers q <= 0; its other half, behind, implies s1 <= 0, so valid needs no q > 0 test.)
+    const double sq = sqrt_core(fabs(t.d));
+    valid = !t.skip && sq > t.h;
+    const uint32_t hi = __double2hiint(sq), lo = __double2loint(sq);
+    const uint32_t shi = (-t.h > sq) ? (hi ^ 0x80000000u) : hi;
+    return -t.h + __hiloint2double(shi, lo);
+  }
+  const double b = 2.0 * t.h;
+  const double sq = sqrt_cr(fabs(t.d));
   const double s0 = (-b - sq) * 0.5;  // == / 2 exactly
   const double s1 = (-b + sq) * 0.5;
-  valid = disc > 0.0 && s1 > 0.0;
+  valid = !t.skip && s1 > 0.0;  // behind (in skip) implies s1 <= 0
   return s0 > 0.0 ? s0 : s1;
 }
-// one sphere; the square root runs only if some lane may hit (skip: disc <= 0 or behind)
-__device__ __forceinline__ double isect_one_sol(double b, double disc, bool skip, bool& valid) {
-  valid = false;
-  double t = 0.0;
-  if (!skip) t = isect_sol(b, disc, valid);
-  return t;
-}
-// two spheres at once; the square roots run only if either test may hit (per lane)
-__device__ __forceinline__ void isect_pair_sol(double b0, double disc0, bool skip0, double b1, double disc1,
-                                               bool skip1, double& t0, bool& v0, double& t1, bool& v1) {
-  v0 = v1 = false;
-  t0 = t1 = 0.0;
-  if (!skip0 || !skip1) {
-    t0 = isect_sol(b0, disc0, v0);
-    t1 = isect_sol(b1, disc1, v1);
+// One sphere / two spheres at once: the square roots run only if some lane may hit, and the
+// consumer f(t, valid[, t1, valid1]) runs inside that branch, so an invalid root is never carried
+// out of it (a placeholder root would cost a move per test; an uninitialised one would be
+// undefined behaviour, which the compiler exploits by deleting the skip test). Lanes outside the
+// branch have no valid root for either sphere.
+template <typename F>
+__device__ __forceinline__ void isect_one(const SphTest& a, F&& f) {
+  if (!a.skip) {
+    bool v;
+    const double t = isect_sol(a, v);
+    f(t, v);
   }
+}
+template <typename F>
+__device__ __forceinline__ void isect_pair(const SphTest& a, const SphTest& b, F&& f) {
+  if (!a.skip || !b.skip) {
+    bool v0, v1;
+    const double t0 = isect_sol(a, v0);
+    const double t1 = isect_sol(b, v1);
+    f(t0, v0, t1, v1);
+  }
+}
+// isect (the reference's root or FARAWAY) through the split test
+template <typename P>
+__device__ __forceinline__ double isect_t(const P* g, double ox, double oy, double oz, double oo, double dx, double dy,
+                                          double dz, double tame) {
+  double r = FARAWAY;
+  isect_one(isect_disc(g, ox, oy, oz, oo, dx, dy, dz, tame), [&](double t, bool v) {
+    if (v) r = t;
+  });
+  return r;
 }
 
 // nearest-hit bookkeeping in scene order (base.py:97-103): the first strictly smaller t wins; an
@@ -485,39 +544,29 @@ __device__ __forceinline__ bool node_may_hit(const cdouble* nd, double ox, doubl
 template <bool CAM, typename Wk>
 __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int cnt, double ox, double oy, double oz,
                                               double oo, double dx, double dy, double dz, double& tmin, int& hit,
-                                              bool& tie, Wk& wk) {
+                                              bool& tie, double tame, Wk& wk) {
   wk.test(cnt);
   const int end = first + cnt;
   int k = first;
   for (; k + 1 < end; k += 2) {
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
     const cdouble* g1 = g0 + RTX_GEOM_WORDS;
-    double b0, d0, b1, d1, t0, t1;
-    bool k0, k1;
-    if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
-      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1, k1);
-    } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
-      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1, k1);
-    }
-    bool v0, v1;
-    isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
-    nearest_update(v0, t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
-    nearest_update(v1, t1, (int)g1[RTX_G_IDX], tmin, hit, tie);
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    const SphTest a1 = CAM ? isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, tame);
+    const int s0 = (int)g0[RTX_G_IDX], s1 = (int)g1[RTX_G_IDX];
+    isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
+      nearest_update(v0, t0, s0, tmin, hit, tie);
+      nearest_update(v1, t1, s1, tmin, hit, tie);
+    });
   }
   if (k < end) {
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
-    double b0, d0;
-    bool k0;
-    if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
-    } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
-    }
-    bool v0;
-    const double t0 = isect_one_sol(b0, d0, k0, v0);
-    nearest_update(v0, t0, (int)g0[RTX_G_IDX], tmin, hit, tie);
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    const int s0 = (int)g0[RTX_G_IDX];
+    isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s0, tmin, hit, tie); });
   }
 }
 
@@ -527,7 +576,7 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
 // is a minimum, `hit` is its unique owner unless tied, and a tie is flagged whatever the order.
 template <bool CAM, typename Wk>
 __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double oy, double oz, double dx, double dy,
-                                            double dz, double& tmin, int& hit, bool& tie, Wk& wk) {
+                                            double dz, double& tmin, int& hit, bool& tie, double tame, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
   const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
@@ -535,7 +584,7 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
   tmin = FARAWAY;
   hit = -1;
   tie = false;
-  nearest_range<CAM>(cg, 0, (int)sc[RTX_H_NALWAYS], ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie, wk);
+  nearest_range<CAM>(cg, 0, (int)sc[RTX_H_NALWAYS], ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie, tame, wk);
   const RaySlab rs = ray_slab(dx, dy, dz, oo);
   int i = 0;
   while (i < nn) {
@@ -543,7 +592,8 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
     wk.node();
     if (__ballot(node_may_hit(nd, ox, oy, oz, rs, tmin)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
-      if (cnt > 0) nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie, wk);
+      if (cnt > 0)
+        nearest_range<CAM>(cg, (int)nd[RTX_N_FIRST], cnt, ox, oy, oz, oo, dx, dy, dz, tmin, hit, tie, tame, wk);
       ++i;
     } else {
       i = (int)nd[RTX_N_SKIP];
@@ -575,12 +625,9 @@ __device__ __forceinline__ void nearest_count_bvh(const cdouble* sc, double ox, 
   auto range = [&](int k, int end) {
     for (; k < end; ++k) {
       const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
-      double b0, d0;
-      bool k0;
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
-      bool v0;
-      const double t0 = isect_one_sol(b0, d0, k0, v0);
-      count_update(v0, t0, (int)g0[RTX_G_IDX], tmin, nh, first);
+      const int s0 = (int)g0[RTX_G_IDX];
+      isect_one(isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, __builtin_nan("")),
+                [&](double t0, bool v0) { count_update(v0, t0, s0, tmin, nh, first); });
     }
   };
   range(0, (int)sc[RTX_H_NALWAYS]);
@@ -604,7 +651,7 @@ __device__ __forceinline__ void nearest_count_bvh(const cdouble* sc, double ox, 
 // Callers guarantee t_self <= FARAWAY in every lane (an invalid test then never shadows).
 template <typename Wk>
 __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
-                                        double ly, double lz, double tself, int hs, Wk& wk) {
+                                        double ly, double lz, double tself, int hs, double tame, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
   const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
@@ -614,12 +661,9 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
     const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
     if ((int)g0[RTX_G_IDX] == hs) continue;
     wk.test(1);
-    double b0, d0;
-    bool k0;
-    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
-    bool v0;
-    const double t0 = isect_one_sol(b0, d0, k0, v0);
-    if (v0 && t0 < tself) lit = false;
+    isect_one(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), [&](double t0, bool v0) {
+      if (v0 && t0 < tself) lit = false;
+    });
   }
   const RaySlab rs = ray_slab(lx, ly, lz, qq);
   int i = 0;
@@ -635,22 +679,16 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
         for (; k + 1 < end; k += 2) {
           const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
           const cdouble* g1 = g0 + RTX_GEOM_WORDS;
-          double b0, d0, b1, d1, t0, t1;
-          bool k0, k1;
-          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
-          isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1, k1);
-          bool v0, v1;
-          isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
-          if ((v0 && t0 < tself) || (v1 && t1 < tself)) lit = false;
+          isect_pair(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame),
+                     isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, tame), [&](double t0, bool v0, double t1, bool v1) {
+                       if ((v0 && t0 < tself) || (v1 && t1 < tself)) lit = false;
+                     });
         }
         if (k < end) {
           const cdouble* g0 = cg + __builtin_amdgcn_readfirstlane(k) * RTX_GEOM_WORDS;
-          double b0, d0;
-          bool k0;
-          isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
-          bool v0;
-          const double t0 = isect_one_sol(b0, d0, k0, v0);
-          if (v0 && t0 < tself) lit = false;
+          isect_one(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), [&](double t0, bool v0) {
+            if (v0 && t0 < tself) lit = false;
+          });
         }
       }
       if (__ballot(lit) == 0) break;  // every lane of the wave is in shadow
@@ -666,7 +704,8 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
 // the scalar cache. CAM: O is the camera (level 0), using the host-precomputed c.
 template <bool CAM, typename P, typename Wk>
 __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, double oy, double oz, double dx,
-                                            double dy, double dz, double& tmin, int& hit, bool& tie, Wk& wk) {
+                                            double dy, double dz, double& tmin, int& hit, bool& tie, double tame,
+                                            Wk& wk) {
   wk.test(nsph);
   tmin = FARAWAY;
   hit = -1;
@@ -676,33 +715,20 @@ __device__ __forceinline__ void nearest_hit(const P* geo, int nsph, double ox, d
   for (; s + 1 < nsph; s += 2) {
     const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
     const P* g1 = g0 + RTX_GEOM_WORDS;
-    double b0, d0, b1, d1;
-    bool k0, k1;
-    if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
-      isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, b1, d1, k1);
-    } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
-      isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, b1, d1, k1);
-    }
-    double t0, t1;
-    bool v0, v1;
-    isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
-    nearest_update(v0, t0, s, tmin, hit, tie);
-    nearest_update(v1, t1, s + 1, tmin, hit, tie);
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    const SphTest a1 = CAM ? isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g1, ox, oy, oz, oo, dx, dy, dz, tame);
+    isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
+      nearest_update(v0, t0, s, tmin, hit, tie);
+      nearest_update(v1, t1, s + 1, tmin, hit, tie);
+    });
   }
   if (s < nsph) {
     const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
-    double b0, d0;
-    bool k0;
-    if (CAM) {
-      isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, b0, d0, k0);
-    } else {
-      isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, b0, d0, k0);
-    }
-    bool v0;
-    const double t0 = isect_one_sol(b0, d0, k0, v0);
-    nearest_update(v0, t0, s, tmin, hit, tie);
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s, tmin, hit, tie); });
   }
 }
 
@@ -931,7 +957,7 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 template <bool IMG = false, typename T, typename G, typename Wk>
 __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* tab, int nsph, int h, double ox,
                                       double oy, double oz, double dx, double dy, double dz, double t, Hit& s,
-                                      Wk& wk) {
+                                      double tame, Wk& wk) {
   const T* gh = tab + h * RTX_GEOM_WORDS;
   const T* mh = tab + nsph * RTX_GEOM_WORDS + h * RTX_MAT_WORDS;
   const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73
@@ -946,7 +972,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
   // Equivalent any-hit form: lit unless some sphere is strictly nearer than the shape itself.
   const double qq = dot3(qx, qy, qz, qx, qy, qz);
-  const double tself = isect(gh, qx, qy, qz, qq, lx, ly, lz);
+  const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
   wk.test(1);
   bool lit = true;
   // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
@@ -958,7 +984,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   const int h0 = __builtin_amdgcn_readfirstlane(h);
   const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
   const bool culled = sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
-  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, wk);
+  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
   const int nshadow = culled ? 0 : nsph - (hs < nsph);
   int j = 0;
   for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
@@ -967,13 +993,12 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
     const G* g0 = geo + j0 * RTX_GEOM_WORDS;
     const G* g1 = geo + j1 * RTX_GEOM_WORDS;
     wk.test(2);
-    double b0, d0, b1, d1, t0, t1;
-    bool k0, k1;
-    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
-    isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, b1, d1, k1);
-    bool v0, v1;
-    isect_pair_sol(b0, d0, k0, b1, d1, k1, t0, v0, t1, v1);
-    if (shadows(v0, t0, tself, far_self) || shadows(v1, t1, tself, far_self)) {
+    bool sh = far_self;  // lanes without a valid root in either test
+    isect_pair(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, tame),
+               [&](double t0, bool v0, double t1, bool v1) {
+                 sh = shadows(v0, t0, tself, far_self) || shadows(v1, t1, tself, far_self);
+               });
+    if (sh) {
       lit = false;
       break;
     }
@@ -981,12 +1006,10 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   if (lit && j < nshadow) {
     const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
     wk.test(1);
-    double b0, d0;
-    bool k0;
-    isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, b0, d0, k0);
-    bool v0;
-    const double t0 = isect_one_sol(b0, d0, k0, v0);
-    if (shadows(v0, t0, tself, far_self)) lit = false;
+    bool sh = far_self;
+    isect_one(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame),
+              [&](double t0, bool v0) { sh = shadows(v0, t0, tself, far_self); });
+    if (sh) lit = false;
   }
 
   const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));  // :138
@@ -1143,6 +1166,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
+  // the half-b sphere test (SphTest): origins the kernel generates itself, in a tame scene
+  const double tame = p.mode != 1 && p.mode != 3 && sc[RTX_H_TAME] != 0.0 ? 0x1.0p-350 : __builtin_nan("");
 
   int64_t i = 0;
   bool active;
@@ -1207,14 +1232,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       hit = p.hit_shape;
     } else if (sc[RTX_H_NNODES] != 0.0) {
       if (cam0) {
-        nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+        nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else {
-        nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+        nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       }
     } else if (cam0) {
-      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     } else {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     }
   }
   if constexpr (LDS) {
@@ -1252,9 +1277,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     Hit s;
     if constexpr (LDS) {
-      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, wk);
+      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
     } else {
-      shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, wk);
+      shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
     }
     if (s.tk < 0) {  // an image-textured sphere: so is this one (the texel lookup stays out of here)
       deferred = true;
@@ -1343,11 +1368,11 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_wave(st, RTX_S_WTRACE + kb + k + 1);
     }
     if (sc[RTX_H_NNODES] != 0.0) {
-      nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+      nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     } else if constexpr (LDS) {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     } else {
-      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, wk);
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     }
   }
 
@@ -1603,7 +1628,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     if (st && d < RTX_S_LEVELS && d > hits_through) stat_add(st, RTX_S_HITS + d, 1);
     Hit s;
     Work<false> nowk;
-    shade<true>(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, nowk);
+    shade<true>(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, __builtin_nan(""), nowk);
     const bool weighted = s.lit && s.g != 0.0;
     bool descend = weighted && (B < 0 || d < B);
     if (descend && d + 1 >= p.stack_levels) {  // deeper than the stack: RecursionError on the host

@@ -226,6 +226,16 @@ def _apply_camera(blob: np.ndarray, cpos, W: int, H: int) -> None:
         geo = t.reshape(S, L.GEOM_WORDS)
         co = (geo[:, L.G_CX] * ox + geo[:, L.G_CY] * oy) + geo[:, L.G_CZ] * oz
         geo[:, L.G_C0] = ((geo[:, L.G_CC] + cw["oo"]) - 2 * co) - geo[:, L.G_RR]
+    h[L.H_TAME] = 1.0 if is_tame(tables[0].reshape(S, L.GEOM_WORDS), cpos) else 0.0
+
+
+def is_tame(geo: np.ndarray, cpos) -> bool:
+    """RTX_H_TAME: every sphere centre coordinate, radius and camera coordinate below 2^60 in
+    magnitude (finite). Origins of every later ray then stay below ~2^140 (hits lie closer than
+    FARAWAY), which the kernel's half-b sphere test relies on (rtx_kernels.hip, SphTest)."""
+    vals = np.concatenate([geo[:, L.G_CX:L.G_CZ + 1].ravel(), 1.0 / geo[:, L.G_INVR],
+                           np.asarray(cpos, dtype=np.float64)])
+    return bool(np.all(np.abs(vals) < L.TAME_BOUND))
 
 
 # --- culling hierarchy ----------------------------------------------------------------------

@@ -342,6 +342,27 @@ def test_fuzz_scenes_against_oracle(hip, seed):
     assert s["rays"] == st.rays and s["hits"] == st.hits, seed
 
 
+@pytest.mark.parametrize("seed", [0, 3, 5])
+def test_untamed_scene_takes_reference_expressions(hip, seed):
+    """A fuzz scene with one sphere beyond 2^60 (RTX_H_TAME = 0): the fast kernel evaluates the
+    reference's sphere-test expressions instead of the half-b form, and still equals the oracle;
+    so does the explicit-ray path on the tamed original."""
+    spec = _fuzz_spec(seed)
+    far = spec["spheres"][0]
+    far["center"] = [3e18, 2e18, 4e19]
+    far["radius"] = 3e18
+    B = 3
+    r, got = _render(hip, spec, B, stats=True)
+    from python_ray_tracer_amd.infrastructure.hip import scene_pack as P
+    assert P.pack_scene(scenes.build_scene(spec))[P.L.H_TAME] == 0.0
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL, (seed, np.abs(got - want).max())
+    W, H = spec["camera"]["width"], spec["camera"]["height"]
+    assert np.array_equal(O.to_uint8(got, W, H), O.to_uint8(want, W, H))
+    assert r.stats()["rays"] == st.rays
+
+
 def test_vector_algebra_on_device(hip):
     """HipVector3D with device tensors (the reference's NumpyVector3D algebra, base.py:28-79) equals
     the NumPy expressions bit for bit, norm's zero guard and sqrt included."""

@@ -43,6 +43,7 @@ def test_abi_layout_matches_header():
     assert const("RTX_H_CAMOO") == L.H_CAMOO
     assert const("RTX_M_TFIOR") == L.M_TFIOR
     assert const("RTX_G_C0") == L.G_C0
+    assert const("RTX_H_TAME") == L.H_TAME
     assert const("RTX_MAGIC") == L.MAGIC
     assert const("RTX_UNBOUNDED_LEVELS") == L.UNBOUNDED_LEVELS
     lay = (ctypes.c_int * 8)()
@@ -323,3 +324,21 @@ def test_pack_image_texture():
     assert blob[L.H_NNODES] > 0  # the tree sits before the texels
     with pytest.raises(ValueError):
         ImageTexture(np.zeros((4, 4)))
+
+
+def test_tame_flag():
+    """RTX_H_TAME (the fast kernel's half-b sphere test): set when every sphere coordinate, radius
+    and camera coordinate is below 2^60 in magnitude, cleared otherwise (and for non-finite ones)."""
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+    from python_ray_tracer_amd.infrastructure.hip import scene_pack as P
+
+    spec = scenes.readme_spec(8, 6)
+    assert P.pack_scene(scenes.build_scene(spec))[L.H_TAME] == 1.0
+    for key, val in (("center", [0.0, 0.0, 2.0 ** 61]), ("radius", 2.0 ** 60)):
+        s2 = scenes.readme_spec(8, 6)
+        s2["spheres"][0][key] = val
+        assert P.pack_scene(scenes.build_scene(s2))[L.H_TAME] == 0.0, key
+    s3 = scenes.readme_spec(8, 6)
+    s3["camera"]["position"] = [0.0, -3e18, 0.0]
+    assert P.pack_scene(scenes.build_scene(s3))[L.H_TAME] == 0.0
