@@ -197,7 +197,9 @@ def main():
 
     traffic = None
     pmc = REPO / "profiles" / "pmc_traffic.json"
-    if pmc.exists():
+    # the PMC figures are whole-frame launches with float32 output on one GPU (tools/gpu_pmc.sh):
+    # a row tile or another output format is a different launch, reported as unmeasured
+    if pmc.exists() and world == 1 and args.out == "f32":
         try:
             d = json.loads(pmc.read_text())
             traffic = d.get(args.config, {}).get("hbm_bytes_per_launch")
