@@ -46,6 +46,8 @@ def _free_port():
 
 
 def _worker(rank, world, port, spec, B, frames, outfile, row_block, sub):
+    # gloo reports its connections on fd 1: keep the parent's stdout (bench.py's one JSON line) clean
+    os.dup2(2, 1)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
