@@ -363,6 +363,23 @@ def test_untamed_scene_takes_reference_expressions(hip, seed):
     assert r.stats()["rays"] == st.rays
 
 
+def test_rays_at_right_angles_take_reference_expressions(hip):
+    """A sphere centred exactly on the camera: every primary ray has h = D.(O - C) = 0, so every
+    wave's half-b test falls back to the reference expressions (SphTest, |h| < 2^-350) at level 0,
+    while the other spheres keep the half-b form; colour, uint8 and counters equal the oracle."""
+    spec = scenes.readme_spec(64, 36)
+    cam = spec["camera"]["position"]
+    spec["spheres"].insert(0, dict(spec["spheres"][0], center=list(cam), radius=0.25))
+    B = 3
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL, np.abs(got - want).max()
+    assert np.array_equal(O.to_uint8(got, 64, 36), O.to_uint8(want, 64, 36))
+    s = r.stats()
+    assert s["rays"] == st.rays and s["hits"] == st.hits
+
+
 def test_vector_algebra_on_device(hip):
     """HipVector3D with device tensors (the reference's NumpyVector3D algebra, base.py:28-79) equals
     the NumPy expressions bit for bit, norm's zero guard and sqrt included."""
