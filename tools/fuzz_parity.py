@@ -1,0 +1,117 @@
+"""Randomised GPU-vs-oracle parity sweep (beyond tests/: many more scenes, small frames).
+
+    python tools/fuzz_parity.py --n 300 [--seed0 5000] [--out gpurun_out/fuzz.json]
+
+Each case draws a scene like tests/test_gpu_parity.py's fuzz generator but wider: 1-40 spheres of
+radius 1e-3 .. 150 (some centred on or touching the camera, some far beyond 2^60 so the scene is
+untamed), random lights, domes, cameras and frame sizes, and a cap in 0..12 or unbounded. The
+HIP render must match the oracle within 1e-12 with identical uint8 pixels and equal per-level
+ray/hit counters. Prints one JSON summary line (and writes it to --out)."""
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+from oracle import numpy_oracle as O  # noqa: E402
+from python_ray_tracer_amd import scenes  # noqa: E402
+
+
+def make_spec(seed, scale=1):
+    rng = np.random.default_rng(seed)
+    n = int(rng.choice([1, 2, 3, 5, 7, 8, 12, 24, 40]))
+    spec = scenes.random_spec(n, seed, int(rng.integers(5, 49)) * scale, int(rng.integers(4, 37)) * scale)
+    cam = [float(v) for v in rng.uniform([-2, -0.4, -6], [2, 2, -0.3])]
+    spec["camera"]["position"] = cam
+    for k, sp in enumerate(spec["spheres"][:-1]):
+        kind = rng.choice(["small", "mid", "big", "oncam", "touch", "far"], p=[0.25, 0.45, 0.1, 0.05, 0.1, 0.05])
+        if kind == "small":
+            sp["radius"] = float(rng.uniform(1e-3, 0.05))
+        elif kind == "mid":
+            sp["radius"] = float(rng.uniform(0.1, 1.5))
+        elif kind == "big":
+            sp["radius"] = 150.0
+            sp["center"] = [float(rng.uniform(-300, 300)), -150.5, float(rng.uniform(160, 400))]
+            continue
+        elif kind == "oncam":  # centred on the camera: every primary ray at right angles
+            sp["center"] = list(cam)
+            sp["radius"] = float(rng.uniform(0.1, 1.0))
+            continue
+        elif kind == "touch":  # the camera on (or within rounding of) the surface
+            r = float(rng.uniform(0.2, 1.0))
+            d = rng.normal(size=3)
+            d /= np.linalg.norm(d)
+            sp["center"] = [float(c + r * v) for c, v in zip(cam, d)]
+            sp["radius"] = r
+            continue
+        else:  # far beyond 2^60: the whole scene is untamed
+            sp["center"] = [float(rng.uniform(-1, 1) * 3e18), float(rng.uniform(0, 1) * 3e18), 4e19]
+            sp["radius"] = 3e18
+            continue
+        sp["center"] = [float(rng.uniform(-4, 4)), float(rng.uniform(-0.5, 3)), float(rng.uniform(0.5, 14))]
+    spec["lights"][0]["position"] = [float(v) for v in rng.uniform([-6, 0.5, -6], [6, 8, 6])]
+    domes = int(rng.integers(0, 3))
+    spec["lights"] = spec["lights"][:1] + [{"kind": "dome", "intensity": float(rng.uniform(0, 0.3)),
+                                            "color": [float(v) for v in rng.uniform(0, 1, 3)]} for _ in range(domes)]
+    B = [0, 1, 2, 3, 3, 4, 5, 6, 8, 12, None][int(rng.integers(0, 11))]
+    return spec, B
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=300)
+    ap.add_argument("--seed0", type=int, default=5000)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--seeds", default=None, help="comma list: only these seeds")
+    ap.add_argument("--scale", type=int, default=1, help="frame size multiplier")
+    a = ap.parse_args()
+    import torch
+
+    from python_ray_tracer_amd.infrastructure import hip as H
+
+    assert torch.cuda.is_available(), "needs a GPU"
+    t0 = time.time()
+    worst, fails, skipped, pixels = 0.0, [], 0, 0
+    seeds = [int(x) for x in a.seeds.split(",")] if a.seeds else [a.seed0 + k for k in range(a.n)]
+    a.n = len(seeds)
+    for k, seed in enumerate(seeds):
+        spec, B = make_spec(seed, a.scale)
+        try:
+            st = O.TraceStats()
+            want = O.render(O.scene_from_spec(spec), B, stats=st)
+        except RecursionError:  # the reference itself fails (>333 levels): nothing to compare
+            skipped += 1
+            continue
+        r = H.HipRenderer(max_bounces=B, collect_stats=True)
+        scene = scenes.build_scene(spec)
+        got = r.raytrace_scene(scene.camera.position, r.get_ray_directions(scene.camera), scene).data.cpu().numpy()
+        W, Hh = spec["camera"]["width"], spec["camera"]["height"]
+        err = float(np.abs(got - want).max())
+        s = r.stats()
+        u8 = np.array_equal(O.to_uint8(got, W, Hh), O.to_uint8(want, W, Hh))
+        # the kernel records the first RTX_S_LEVELS (64) levels; longer unbounded chains stop there
+        cnt = s["rays"] == st.rays[:64] and s["hits"] == st.hits[:64]
+        ok = err <= 1e-12 and u8 and cnt
+        worst = max(worst, err)
+        pixels += W * Hh
+        if not ok:
+            fails.append({"seed": seed, "B": B, "err": err, "uint8_equal": bool(u8), "counters_equal": bool(cnt),
+                          "rays": [s["rays"], st.rays] if not cnt else None,
+                          "hits": [s["hits"], st.hits] if not cnt else None})
+        if k % 50 == 49:
+            print(f"{k + 1} cases, {len(fails)} failures, worst {worst:.3g}", file=sys.stderr, flush=True)
+    res = {"cases": a.n, "scale": a.scale, "compared": a.n - skipped, "skipped_reference_recursion_error": skipped,
+           "pixels": pixels, "failures": fails, "worst_abs_err": worst, "seconds": round(time.time() - t0, 1)}
+    line = json.dumps(res)
+    print(line)
+    if a.out:
+        Path(a.out).write_text(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
