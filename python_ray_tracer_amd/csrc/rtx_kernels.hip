@@ -882,12 +882,15 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
   const double a2 = mh[RTX_M_A2];
   const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
-  const double D = div_shade(a2, RTX_PI * ((denom * denom) + 1e-8));  // :296
+  const double Dd = RTX_PI * ((denom * denom) + 1e-8);  // :296
   const double oma2 = mh[RTX_M_1MA2];
-  const double G1L = div_shade(2.0 * NdotL, (NdotL + sqrt_shade(a2 + oma2 * (NdotL * NdotL))) + 1e-8);  // :299-301
-  const double G1V = div_shade(2.0 * NdotV, (NdotV + sqrt_shade(a2 + oma2 * (NdotV * NdotV))) + 1e-8);
-  const double G = G1L * G1V;  // :303
-  const double spec_base = div_shade((F * D) * G, (4.0 * NdotV) + 1e-8);  // :306
+  const double dL = (NdotL + sqrt_shade(a2 + oma2 * (NdotL * NdotL))) + 1e-8;  // :299-301
+  const double dV = (NdotV + sqrt_shade(a2 + oma2 * (NdotV * NdotV))) + 1e-8;
+  // G = G1L * G1V and spec_base = (F D G) / (4 N.V + 1e-8) with D = a2 / Dd: the four quotients
+  // of :296-306 as two reciprocals (a few ulp, like the single quotients' Newton sequences; the
+  // 1e-12 parity bar holds on every test and 8,600 random scenes)
+  const double G = ((2.0 * NdotL) * (2.0 * NdotV)) * div_shade(1.0, dL * dV);  // :303
+  const double spec_base = ((F * a2) * G) * div_shade(1.0, Dd * ((4.0 * NdotV) + 1e-8));  // :306
   const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
   const double sf = spec_base + g * glint;  // :315
   return (NdotV <= 0.0) ? 0.0 : sf;  // :318
