@@ -110,6 +110,7 @@ __host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)lev
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
+constexpr size_t kLdsBytesPerCu = 160 * 1024;  // gfx950
 
 // Wave-uniform loads through the scalar cache: the constant address space makes hipcc emit s_load
 // even though the kernel also stores (it cannot prove the scene blob is not aliased otherwise).
@@ -1974,7 +1975,15 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
         launch_fast_lds<B, true, false>(p, grid, s);
       }
     } else {
-      launch_fast_lds<B, false, levels_in_lds<B, true, false>()>(p, grid, s);
+      // caps 3-4 in big scenes: three LDS level slots beside a large scene table leave room for
+      // fewer than 4 blocks per CU; the register-level kernel (128 VGPRs, 4 waves/SIMD) then runs
+      // more waves than the LDS-slot kernel can
+      constexpr bool kTry = B == 3 || B == 4;
+      if (kTry && (size_t)p.nsph * kSphWords * sizeof(double) + level_lds_bytes(B) > kLdsBytesPerCu / 4) {
+        if constexpr (kTry) launch_fast_lds<B, false, false>(p, grid, s);
+      } else {
+        launch_fast_lds<B, false, levels_in_lds<B, true, false>()>(p, grid, s);
+      }
     }
   } else {
     if (p.stats) {

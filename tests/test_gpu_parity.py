@@ -380,6 +380,20 @@ def test_rays_at_right_angles_take_reference_expressions(hip):
     assert s["rays"] == st.rays and s["hits"] == st.hits
 
 
+@pytest.mark.parametrize("B", [3, 4])
+def test_big_scene_register_level_kernel(hip, B):
+    """65 spheres at caps 3 and 4: the LDS-slot kernel would fit 3 blocks per CU beside the scene
+    table, so the register-level kernel renders it (launch_fast_b); colour, uint8 and counters."""
+    spec = scenes.random_spec(64, 3, 96, 54)
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL, np.abs(got - want).max()
+    assert np.array_equal(O.to_uint8(got, 96, 54), O.to_uint8(want, 96, 54))
+    s = r.stats()
+    assert s["rays"] == st.rays and s["hits"] == st.hits
+
+
 def test_vector_algebra_on_device(hip):
     """HipVector3D with device tensors (the reference's NumpyVector3D algebra, base.py:28-79) equals
     the NumPy expressions bit for bit, norm's zero guard and sqrt included."""
