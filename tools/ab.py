@@ -43,10 +43,13 @@ def main():
     ap.add_argument("--no-events", action="store_true", help="end-to-end only: no per-launch kernel events")
     ap.add_argument("--bvh-leaf", type=int, default=None, help="override scene_pack.BVH_LEAF (spheres per leaf)")
     ap.add_argument("--bounces", type=int, default=None, help="override the config's bounce cap (-1: unbounded)")
+    ap.add_argument("--spheres", type=int, default=None, help="a seeded random scene of this many spheres at the config's size")
     a = ap.parse_args()
     spec, B = scenes.CONFIGS[a.config]()
     if a.bounces is not None:
         B = a.bounces
+    if a.spheres is not None:
+        spec = scenes.random_spec(a.spheres, 0, spec["camera"]["width"], spec["camera"]["height"])
     if a.bvh_leaf is not None:
         from python_ray_tracer_amd.infrastructure.hip import scene_pack
 
