@@ -516,3 +516,16 @@ def test_image_textured_spheres(hip, B):
     r2 = hip.HipRenderer(max_bounces=B)
     got2 = r2.render(scene2).data.cpu().numpy()
     assert np.abs(got2 - got).max() <= ATOL
+
+
+@pytest.mark.parametrize("B", [3, None])
+def test_textured_batch_matches_single_frames(hip, B):
+    """A multi-frame launch (rtx_render_frames) of an orbit around the textured scene: the
+    image-textured hits of every frame go to the general kernel with their frame index (its
+    waterfall over frames), and each frame equals its single-frame render bit for bit."""
+    base = _textured_spec(64, 36)
+    frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 6))) for k in range(4)]
+    r = hip.HipRenderer(max_bounces=B)
+    batch = r.render_batch(frames)
+    for f, sc in enumerate(frames):
+        assert torch.equal(batch[f], r.render_tile(sc)), (B, f)
