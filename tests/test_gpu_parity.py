@@ -529,3 +529,23 @@ def test_textured_batch_matches_single_frames(hip, B):
     batch = r.render_batch(frames)
     for f, sc in enumerate(frames):
         assert torch.equal(batch[f], r.render_tile(sc)), (B, f)
+
+
+@pytest.mark.parametrize("B", [3, None])
+def test_textured_row_tiles_reassemble(hip, B):
+    """Row tiles of the textured scene (its image-textured hits deferred from each tile to the
+    general kernel, which maps the tile's local pixel back to its frame row): reassembled they equal
+    the whole frame bit for bit."""
+    from python_ray_tracer_amd import tiling
+
+    spec = _textured_spec(96, 61)
+    scene = scenes.build_scene(spec)
+    r = hip.HipRenderer(max_bounces=B)
+    full = r.render(scene).data
+    for P, rb in ((3, 4), (4, 8)):
+        n = tiling.part_len(61, 96, rb, P, full.element_size(), None)
+        buf = torch.zeros((P, n), dtype=full.dtype, device=full.device)
+        for p in range(P):
+            shp = tiling.tile_shape(61, 96, rb, P, p, None)
+            r.render_tile(scene, rb, P, p, into=buf[p, :int(np.prod(shp))].view(shp))
+        assert torch.equal(r.assemble_rows(buf, 96, 61, rb, None), full), (B, P, rb)
