@@ -7,10 +7,13 @@ camera.position, get_ray_directions(camera), scene)``: scene packing (cached by 
 ray generation, nearest hit, shadow rays, shading and every reflection level up to the cap, with the
 unclipped colour left in HBM (float32 [3, W*H]). PNG encoding is not part of a step.
 
-Default workload (N=1): BASELINE.json configs[1] — the README scene at 1920x1080, 3 reflection
-bounces. ``--mode frames`` (default, weak scaling): every rank renders its own frames, no collective
-in the loop (the frame sharding of config C5). ``--mode tiles`` (strong scaling): every rank renders
-its interleaved row tile of ONE frame and the tiles are gathered to rank 0 (RCCL) every step.
+Default workload: BASELINE.json configs[1] — the README scene at 1920x1080, 3 reflection bounces.
+``--mode frames`` (the default at every N, weak scaling): every rank renders whole frames, no
+collective in the loop (the frame sharding of config C5), so N=1 and N>1 lines measure
+the same code path and output format. ``--mode tiles`` (strong scaling): every rank renders its
+interleaved row tile of ONE frame and the uint8 tiles are gathered to rank 0 (RCCL) every step; the
+default line carries it at every N as ``secondary.tiles_u8`` (the config) and ``secondary.c4_tiles``
+(C4, 7680x4320), on a one-rank process group at N=1.
 
 Timing: W untimed warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
 The dominant kernel's own time is measured live with HIP events recorded by the library on the
@@ -42,14 +45,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2", help="C1|C2|C2main|C3|C4|C5 (python_ray_tracer_amd/scenes.py)")
-    ap.add_argument("--mode", default=None, choices=["frames", "tiles"],
-                    help="default: frames at N=1, tiles (row tiles + RCCL gather of one frame) at N>1")
+    ap.add_argument("--mode", default="frames", choices=["frames", "tiles"],
+                    help="frames (default: every rank renders whole frames, weak scaling) or tiles (row tiles + "
+                         "RCCL gather of one frame, strong scaling)")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--out", default=None, choices=["f32", "f64", "u8"],
-                    help="frame format left in HBM (default f32; u8 in tiles mode at N>1: the gathered frame is "
-                         "the uint8 image save_image writes)")
+                    help="frame format left in HBM (default f32; u8 in tiles mode: the gathered frame is the "
+                         "uint8 image save_image writes)")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="N>1: skip the extra weak-scaling frames and C4-tiles measurements")
+                    help="skip the tiles-mode (row tiles + gather) measurements of the config and of C4")
     ap.add_argument("--cpu-procs", type=int, default=14,
                     help="processes of the row-tiled all-cores CPU baseline (the box's CPU share is 16 cores, and "
                          "at most 16 processes may hold the GPU open: importing torch opens it in every worker, "
@@ -64,6 +68,10 @@ def parse():
     ap.add_argument("--prof-every", type=int, default=10,
                     help="time the dominant kernel with HIP events on one launch in this many (timing a launch "
                          "costs stream time; 1 = every launch)")
+    ap.add_argument("--emulate-parts", default=None, metavar="N,N,...",
+                    help="one GPU: time every part p of render_tile(scene, row_block, N, p) for each N (the compute "
+                         "side of the N-GPU row-tiled frame) and assemble_rows of N parts; prints one JSON line "
+                         "(metric: per-part kernel time) instead of the bench line")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -71,11 +79,8 @@ def parse():
 
 def main():
     args = parse()
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.mode is None:
-        args.mode = "tiles" if world_env > 1 else "frames"
     if args.out is None:
-        args.out = "u8" if (args.mode == "tiles" and world_env > 1) else "f32"
+        args.out = "u8" if args.mode == "tiles" else "f32"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -111,6 +116,13 @@ def main():
     scene = scenes.build_scene(spec)
     dtype = torch.float64 if args.out == "f64" else torch.float32
     r = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev)
+
+    if args.emulate_parts:
+        line = emulate_parts(args, r, scene, spec, B, [int(v) for v in args.emulate_parts.split(",")])
+        print(json.dumps(line))
+        if args.json_out:
+            Path(args.json_out).write_text(json.dumps(line) + "\n")
+        return
 
     F = max(1, args.frames_per_step)
     if args.mode == "frames" and F > 1:
@@ -194,6 +206,11 @@ def main():
     achieved_tflops = flops / kern_avg_s / 1e12
     achieved_exec = flops_exec / kern_avg_s / 1e12
     achieved_gbs = alg_bytes / kern_avg_s / 1e9
+    # A scene with a culling tree (C3, C4, C5) skips most of the tests the reference performs: the
+    # headline fraction is then the executed-work one (the kernel's efficiency), and the §8d figure,
+    # which prices every reference test, is kept as reference_equivalent.
+    culled = st["node_tests"] > 0
+    head_tflops, head_flops = (achieved_exec, flops_exec) if culled else (achieved_tflops, flops)
 
     traffic = None
     pmc = REPO / "profiles" / "pmc_traffic.json"
@@ -209,16 +226,13 @@ def main():
     out_path = output_path_times(r, scene) if rank == 0 else None
 
     secondary = None
-    if world > 1 and not args.no_secondary:
-        secondary = secondary_measurements(args, r, spec, B, scene, world, rank, dev, coll_dev, barrier)
+    if not args.no_secondary and args.frames_per_step == 1 and args.mode == "frames":
+        secondary = secondary_tiles(args, r, scene, world, dev, coll_dev)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(spec, B, args.cpu_seconds)
-        try:
-            cpu = cpu_baseline_all_cores(spec, B, args.cpu_procs, args.cpu_seconds, cpu)
-        except Exception as e:  # noqa: BLE001 - the baseline is reported, never fatal
-            cpu["all_cores_error"] = repr(e)[:300]
+        cpu = cpu_baseline_or_error(spec, B, args.cpu_procs, args.cpu_seconds, cpu)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -251,14 +265,20 @@ def main():
             "roofline": {
                 "bound": "valu",
                 "kernel": f"k_render_fast<{B}>" if B is not None and B <= 6 else "k_render_fast<5, DEEP> (first pass)",
-                "achieved": round(achieved_tflops, 4),
+                "achieved": round(head_tflops, 4),
                 "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / PEAK_FP64_TFLOPS, 5),
+                "frac": round(head_tflops / PEAK_FP64_TFLOPS, 5),
                 "traffic": traffic,
                 "kernel_ms": round(kern_avg_s * 1e3, 5),
                 "kernel_launches_timed": kern_n,
-                "flops_per_launch": flops,
+                "flops_per_launch": head_flops,
+                "flops_model": "executed (culling tree: tests the kernel ran)" if culled else "SURVEY.md 8d",
+                "reference_equivalent": {
+                    "achieved": round(achieved_tflops, 4), "frac": round(achieved_tflops / PEAK_FP64_TFLOPS, 5),
+                    "flops_per_launch": flops,
+                    "note": "the SURVEY.md 8d model: every ray tests all S spheres, as the reference does (culled "
+                            "tests priced too: reference-equivalent throughput, not kernel efficiency)"},
                 "executed_model": {
                     "achieved": round(achieved_exec, 4), "frac": round(achieved_exec / PEAK_FP64_TFLOPS, 5),
                     "flops_per_launch": flops_exec, "sphere_tests": st["sphere_tests"],
@@ -276,7 +296,7 @@ def main():
                 "hbm": {"achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "alg_bytes_per_launch": alg_bytes},
                 "note": "FP64 VALU-bound megakernel (no dense contraction, no MFMA); achieved = algorithmic "
-                        "FLOPs (SURVEY.md 8d model, kernel counters) / kernel time (HIP events on the launch "
+                        "FLOPs (flops_model, kernel counters) / kernel time (HIP events on the launch "
                         f"stream around 1 in {every} launches of the timed region)",
             },
             "cpu_baseline": cpu,
@@ -298,12 +318,13 @@ def main():
 
 
 def tiles_stepper(r, scene, world, row_block, out):
-    """(step, drain) of the strong-scaling tiles mode. World 1: the whole frame rendered into a
-    pre-allocated buffer. World > 1: TileGather with two slots; step k submits frame k and
-    finishes frame k-1 (its gather overlapped frame k's render); drain finishes the last one."""
+    """(step, drain) of the strong-scaling tiles mode: TileGather with two slots; step k submits
+    frame k and finishes frame k-1 (its gather overlapped frame k's render); drain finishes the last
+    one. Without a process group: the whole frame rendered into a pre-allocated buffer."""
     import torch
+    import torch.distributed as dist
 
-    if world == 1:
+    if not dist.is_initialized():  # one process without a group: the whole frame, no gather
         W, H = int(scene.camera.width), int(scene.camera.height)
         buf = (torch.empty((H, W, 3), dtype=torch.uint8, device=r.device) if out == "u8"
                else torch.empty((3, W * H), dtype=r.color_dtype, device=r.device))
@@ -331,16 +352,42 @@ def tiles_stepper(r, scene, world, row_block, out):
     return step, drain
 
 
-def secondary_measurements(args, r, spec, B, scene, world, rank, dev, coll_dev, barrier):
-    """N > 1 extras on the same ranks, each timed like the headline (barrier, K steps, barrier,
-    max over ranks): (1) weak scaling, every rank renders whole frames of the config with no
-    collective (the frame sharding of C5); (2) the C4 scaling config (7680x4320, 65 spheres, B=5)
-    in tiles mode with the uint8 gather."""
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def secondary_tiles(args, r, scene, world, dev, coll_dev):
+    """The strong-scaling row-tiled frame next to the headline, at every N:
+    tiles mode — every rank renders its interleaved row tile into the gather buffer, the gather to
+    rank 0, rtx_assemble_rows there, uint8 frame, two frames in flight (distributed.TileGather) — for
+    the config and for C4 (7680x4320, the scaling config). At N=1 on a one-rank process group, so
+    the N=1 point runs the same code as N>1. Timed like the headline (barrier, K steps, barrier,
+    max over ranks); never fatal."""
     import torch
     import torch.distributed as dist
 
     from python_ray_tracer_amd import scenes
     from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    own_group = False
+    try:
+        if not dist.is_initialized():
+            kw = {"device_id": dev} if args.backend == "nccl" else {}
+            dist.init_process_group(args.backend, init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                                    world_size=1, **kw)
+            own_group = True
+    except Exception as e:  # noqa: BLE001 - a secondary measurement, never fatal
+        return {"tiles_error": repr(e)[:300]}
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
 
     def timed(step, drain, k, warm):
         for _ in range(warm):
@@ -353,36 +400,126 @@ def secondary_measurements(args, r, spec, B, scene, world, rank, dev, coll_dev, 
         drain()
         barrier()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    W, H = spec["camera"]["width"], spec["camera"]["height"]
     out = {}
-    k = max(10, min(args.steps, 100))
-
-    def frame_step():
-        return r.render_tile(scene, out="u8" if args.out == "u8" else None)
-    t = timed(frame_step, lambda: None, k, 3)
-    out["frames_weak"] = {"value": round(world * W * H * k / t / 1e6, 3), "unit": "Mpixels/s",
-                          "ms_per_step": round(t / k * 1e3, 5), "steps": k, "scaling": "weak",
-                          "config": f"{args.config}, every rank renders whole frames, no collective"}
-    c4spec, c4B = scenes.CONFIGS["C4"]()
-    c4 = scenes.build_scene(c4spec)
-    r4 = HipRenderer(max_bounces=c4B, color_dtype=torch.float32, device=dev)
-    step, drain = tiles_stepper(r4, c4, world, args.row_block, "u8")
-    k4 = 10
-    t = timed(step, drain, k4, 2)
-    out["c4_tiles"] = {"value": round(7680 * 4320 * k4 / t / 1e6, 3), "unit": "Mpixels/s",
-                       "ms_per_step": round(t / k4 * 1e3, 5), "steps": k4, "scaling": "strong",
-                       "config": "C4: 64 random spheres + ground 7680x4320 seed 0, 5 bounces, row tiles "
-                                 f"(row_block {args.row_block}) + gather of the uint8 frame to rank 0"}
+    try:
+        W, H = int(scene.camera.width), int(scene.camera.height)
+        k = max(10, min(args.steps, 200))
+        step, drain = tiles_stepper(r, scene, world, args.row_block, "u8")
+        t = timed(step, drain, k, 5)
+        out["tiles_u8"] = {"value": round(W * H * k / t / 1e6, 3), "unit": "Mpixels/s",
+                           "ms_per_step": round(t / k * 1e3, 5), "steps": k, "scaling": "strong",
+                           "config": f"{args.config} row-tiled over {world} rank(s) ({dist.get_backend()}): render "
+                                     f"into the gather buffer (row_block {args.row_block}), gather to rank 0, "
+                                     "rtx_assemble_rows, uint8 frame, two frames in flight"}
+        c4spec, c4B = scenes.CONFIGS["C4"]()
+        r4 = HipRenderer(max_bounces=c4B, color_dtype=torch.float32, device=dev)
+        step, drain = tiles_stepper(r4, scenes.build_scene(c4spec), world, args.row_block, "u8")
+        k4 = 10
+        t = timed(step, drain, k4, 2)
+        out["c4_tiles"] = {"value": round(7680 * 4320 * k4 / t / 1e6, 3), "unit": "Mpixels/s",
+                           "ms_per_step": round(t / k4 * 1e3, 5), "steps": k4, "scaling": "strong",
+                           "config": "C4: 64 random spheres + ground 7680x4320 seed 0, 5 bounces, row-tiled over "
+                                     f"{world} rank(s), gather of the uint8 frame to rank 0"}
+    except Exception as e:  # noqa: BLE001
+        out["tiles_error"] = repr(e)[:300]
+    finally:
+        if own_group:
+            dist.destroy_process_group()
     return out
 
 
-def cpu_baseline_all_cores(spec, B, procs, budget_s, single):
+def emulate_parts(args, r, scene, spec, B, part_counts):
+    """The compute side of the N-GPU row-tiled frame on one GPU: for each N,
+    every part p of render_tile(scene, row_block, N, p) is rendered into its slot of an [N,
+    part_len] uint8 gather buffer, as rank p would, and timed — the fast kernel by the library's HIP
+    events, the whole launch (fast + general kernel, host call) by wall clock over K synchronised
+    launches — then rtx_assemble_rows of the N parts (the root's un-permute), whose frame must equal
+    the single-GPU render. The gather itself is not emulated: DESIGN.md §6 prices it from the part
+    bytes reported here."""
+    import numpy as np
+    import torch
+
+    from python_ray_tracer_amd import tiling
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    W, H = int(scene.camera.width), int(scene.camera.height)
+    dev = r.device
+    rb = args.row_block
+    k = max(5, min(args.steps, 100))
+
+    def kernel_us(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        L.profile_sample(1)
+        L.profile_enable(k)
+        for _ in range(k):
+            fn()
+        ms, n = L.profile_collect()
+        L.profile_enable(0)
+        return ms / max(n, 1) * 1e3
+
+    def wall_us(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / k * 1e6
+
+    whole = r.render_tile(scene, out="u8")
+    res = {}
+    for N in sorted({1, *part_counts}):
+        plen = tiling.part_len(H, W, rb, N, 1, "u8")
+        tiles = torch.zeros((N, plen), dtype=torch.uint8, device=dev)
+        parts = []
+        for p in range(N):
+            shp = tiling.tile_shape(H, W, rb, N, p, "u8")
+            view = tiles[p, :int(np.prod(shp))].view(shp)
+
+            def fn(p=p, view=view):
+                return r.render_tile(scene, rb, N, p, out="u8", into=view)
+            parts.append({"part": p, "rows": shp[0], "kernel_us": round(kernel_us(fn), 3),
+                          "launch_us": round(wall_us(fn), 3)})
+        frame = r.assemble_rows(tiles, W, H, rb, "u8")
+        if not torch.equal(frame, whole):
+            raise AssertionError(f"assembled {N}-part frame differs from the whole-frame render")
+        asm_us = wall_us(lambda: r.assemble_rows(tiles, W, H, rb, "u8"))
+        kus = [q["kernel_us"] for q in parts]
+        lus = [q["launch_us"] for q in parts]
+        res[str(N)] = {"kernel_us_max": max(kus), "kernel_us_mean": round(sum(kus) / N, 3),
+                       "imbalance": round(max(kus) / (sum(kus) / N), 4), "launch_us_max": max(lus),
+                       "assemble_us": round(asm_us, 3), "part_bytes": plen, "root_receives_bytes": (N - 1) * plen,
+                       "frame_equals_single_gpu": True, "parts": parts}
+    return {"metric": "per-part row-tile render time, 1-GPU emulation of the N-GPU frame", "unit": "us",
+            "config": {"workload": args.config, "width": W, "height": H, "max_bounces": B,
+                       "spheres": len(spec["spheres"]), "row_block": rb, "output": "u8", "launches_per_part": k},
+            "n": res,
+            "note": "kernel_us: k_render_fast by HIP events (library); launch_us: one render_tile call end to end "
+                    "(fast + general kernel and the host call), K synchronised calls; assemble_us: "
+                    "rtx_assemble_rows of the N parts on the root"}
+
+
+def cpu_baseline_or_error(spec, B, procs, budget_s, single, timeout_s=None):
+    """cpu_baseline_all_cores, or the 1-core baseline with ``all_cores_error`` when the all-cores
+    leg fails or times out: the baseline is reported, never fatal."""
+    try:
+        return cpu_baseline_all_cores(spec, B, procs, budget_s, single, timeout_s)
+    except Exception as e:  # noqa: BLE001
+        out = dict(single)
+        out["all_cores_error"] = repr(e)[:300]
+        return out
+
+
+def cpu_baseline_all_cores(spec, B, procs, budget_s, single, timeout_s=None):
     """The oracle row-tiled over ``procs`` processes (one core each) through the gloo multi-rank
     path (oracle/row_tiled.py): render + gather of whole frames (frames up to 2.5 Mpixels) or of
-    a sample of interleaved row tiles (C3, C4). ``single``: the 1-core result, kept beside it."""
+    a sample of interleaved row tiles (C3, C4). ``single``: the 1-core result, kept beside it.
+    Runs in a child process group killed after ``timeout_s`` (raises TimeoutError)."""
     import math
 
     from oracle import row_tiled
@@ -392,7 +529,10 @@ def cpu_baseline_all_cores(spec, B, procs, budget_s, single):
     sub = 1 if W * H <= 2_500_000 else math.ceil(W * H / (procs * 600_000))
     t_step = W * H / sub / (single["value"] * 1e6) / procs * 1.3  # estimated wall time of one step
     frames = int(max(2, min(20, budget_s / max(t_step, 1e-3))))
-    res = row_tiled.time_row_tiled(spec, B, procs, frames=frames, sub=sub)
+    # in a child process group with a hard limit: a stuck gloo rendezvous cannot hold the JSON line
+    # back (start-up and imports of the workers take ~10-20 s on a fresh box)
+    limit = timeout_s if timeout_s is not None else 90.0 + 3.0 * frames * t_step
+    res = row_tiled.run_bounded(spec, B, procs, frames, sub, limit)
     rate = max(p / t for p, t in zip(res["pixels"], res["times"]))
     what = (f"{frames} full {W}x{H} frames" if sub == 1 else
             f"{frames} samples of {procs} interleaved row tiles (1/{sub} of the {W}x{H} frame each)")

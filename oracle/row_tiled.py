@@ -58,6 +58,8 @@ def _worker(rank, world, port, spec, B, frames, outfile, row_block, sub):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        if os.environ.get("ROW_TILED_STALL_RANK") == str(rank):  # test hook: a stuck worker (tests/)
+            time.sleep(3600)
         scene = scenes.build_scene(spec)
         r = OracleTileRenderer(B)
         times, pixels = [], []
@@ -92,7 +94,9 @@ def time_row_tiled(spec: dict, max_bounces, procs: int, frames: int = 3, row_blo
     sample instead of whole frames: each step, every process renders one part of a
     (procs * sub)-way interleaved split (1/sub of the frame in total). Returns
     {"times": [...], "pixels": [...]} per step."""
-    import torch.multiprocessing as mp
+    # stdlib multiprocessing (spawn): this process itself never imports torch, so under
+    # run_bounded only the workers hold the GPU runtime open (the box allows 16 such processes)
+    import multiprocessing as mp
 
     old = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
     for k in old:
@@ -100,8 +104,17 @@ def time_row_tiled(spec: dict, max_bounces, procs: int, frames: int = 3, row_blo
     try:
         with tempfile.TemporaryDirectory() as d:
             out = os.path.join(d, "times.json")
-            mp.start_processes(_worker, args=(procs, _free_port(), spec, max_bounces, frames, out, row_block, sub),
-                               nprocs=procs, start_method="spawn", join=True)
+            ctx = mp.get_context("spawn")
+            port = _free_port()
+            ps = [ctx.Process(target=_worker, args=(r, procs, port, spec, max_bounces, frames, out, row_block, sub))
+                  for r in range(procs)]
+            for p in ps:
+                p.start()
+            for p in ps:
+                p.join()
+            bad = [(r, p.exitcode) for r, p in enumerate(ps) if p.exitcode != 0]
+            if bad:
+                raise RuntimeError(f"row-tiled workers failed (rank, exit code): {bad}")
             with open(out) as f:
                 return json.load(f)
     finally:
@@ -112,9 +125,58 @@ def time_row_tiled(spec: dict, max_bounces, procs: int, frames: int = 3, row_blo
                 os.environ[k] = v
 
 
+def run_bounded(spec: dict, max_bounces, procs: int, frames: int, sub: int, timeout_s: float,
+                row_block: int = 8) -> dict:
+    """time_row_tiled in a child process (its own session) with a hard time limit: a worker stuck in
+    the gloo rendezvous or the gather cannot hang the caller (bench.py's cpu_baseline leg). On
+    timeout the child's whole process group — the child and its spawned workers — is killed and
+    TimeoutError raised."""
+    import signal
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as d:
+        args = os.path.join(d, "args.json")
+        out = os.path.join(d, "out.json")
+        with open(args, "w") as f:
+            json.dump({"spec": spec, "B": max_bounces, "procs": procs, "frames": frames, "sub": sub,
+                       "row_block": row_block, "out": out}, f)
+        # stdout to stderr: the caller's stdout carries bench.py's one JSON line
+        p = subprocess.Popen([sys.executable, "-m", "oracle.row_tiled", args], cwd=repo, stdout=sys.stderr,
+                             start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)  # the group this call created (start_new_session)
+            p.wait()
+            raise TimeoutError(f"row-tiled CPU baseline exceeded {timeout_s:.0f}s; its process group was killed")
+        if rc != 0:
+            raise RuntimeError(f"row-tiled CPU baseline exited with {rc}")
+        with open(out) as f:
+            return json.load(f)
+
+
+def _main(argv) -> None:
+    # through the importable module, so the spawned workers unpickle oracle.row_tiled._worker
+    from oracle.row_tiled import time_row_tiled
+
+    with open(argv[0]) as f:
+        a = json.load(f)
+    res = time_row_tiled(a["spec"], a["B"], a["procs"], frames=a["frames"], row_block=a["row_block"], sub=a["sub"])
+    with open(a["out"], "w") as f:
+        json.dump(res, f)
+
+
 def host_cores() -> int:
     """CPUs this process may run on (the GPU box shares a large host: its cgroup/affinity share)."""
     try:
         return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):  # pragma: no cover
         return os.cpu_count() or 1
+
+
+if __name__ == "__main__":
+    import sys
+
+    _main(sys.argv[1:])

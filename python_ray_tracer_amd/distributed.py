@@ -88,9 +88,17 @@ class TileGather:
         return self.finish(0)
 
 
+# TileGathers cached per renderer (one per frame size / tiling / group / output). Each holds a send
+# buffer and, on the root, world x part_len receive buffers (C4 on 8 ranks: ~100 MB of uint8 tiles
+# on the root), so the cache is small and evicts the least recently used entry.
+TILE_GATHER_CACHE = 4
+
+
 def tile_gather_for(renderer, scene, *, group=None, row_block: int = 8, dst: int = 0, out=None) -> TileGather:
     """The renderer's cached TileGather for this frame size, tiling and group (buffers persist
-    across calls, so a frame sequence allocates nothing per frame)."""
+    across calls, so a frame sequence allocates nothing per frame). One slot: the synchronous
+    render_frame_distributed path never has two frames in flight (bench.py's pipelined tiles mode
+    builds its own two-slot TileGather)."""
     import torch.distributed as dist
 
     W, H = int(scene.camera.width), int(scene.camera.height)
@@ -103,7 +111,10 @@ def tile_gather_for(renderer, scene, *, group=None, row_block: int = 8, dst: int
             renderer._tile_gathers = cache
         except AttributeError:  # pragma: no cover - renderer without a __dict__
             pass
-    tg = cache.get(key)
+    tg = cache.pop(key, None)
     if tg is None:
-        tg = cache[key] = TileGather(renderer, W, H, group=group, row_block=row_block, dst=dst, out=out)
+        while len(cache) >= TILE_GATHER_CACHE:
+            cache.pop(next(iter(cache)))  # least recently used (dicts keep insertion order)
+        tg = TileGather(renderer, W, H, group=group, row_block=row_block, dst=dst, out=out, slots=1)
+    cache[key] = tg  # most recently used last
     return tg

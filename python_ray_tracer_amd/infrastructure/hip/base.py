@@ -187,6 +187,19 @@ class HipCameraRays(HipVectorArray3D):
 _OUT_KIND = {torch.float32: L.OUT_F32_SOA, torch.float64: L.OUT_F64_SOA}
 
 
+def _on_device(method):
+    """Run a launching method with the renderer's device current: the library sizes grids by the
+    current device's CUs and occupancy and launches there, so a HipRenderer(device="cuda:1") must
+    not depend on which device the caller made current."""
+    import functools
+
+    @functools.wraps(method)
+    def run(self, *args, **kwargs):
+        with torch.cuda.device(self.device):
+            return method(self, *args, **kwargs)
+    return run
+
+
 class HipRenderer(Renderer):
     """MI355X renderer behind the reference ``Renderer`` plugin surface (application.py:7-32)."""
 
@@ -272,6 +285,7 @@ class HipRenderer(Renderer):
         """get_ray_directions + raytrace_scene of the scene camera (application.py:48-50), fused."""
         return HipRGBColor.from_tensor(self.render_tile(scene))
 
+    @_on_device
     def render_tile(self, scene, row_block: int = 1, n_parts: int = 1, part: int = 0, out: str | None = None,
                     blob: torch.Tensor | None = None, n_spheres: int | None = None,
                     into: torch.Tensor | None = None) -> torch.Tensor:
@@ -311,6 +325,7 @@ class HipRenderer(Renderer):
         self._check_status(ws)
         return res
 
+    @_on_device
     def render_batch(self, scenes, out: str | None = None) -> torch.Tensor:
         """Whole frames of several scenes in ONE launch (rtx_render_frames).
         All scenes need the same camera size and sphere count; cameras, spheres and lights may
@@ -355,6 +370,7 @@ class HipRenderer(Renderer):
             self._scene_cache[ck] = hit
         return ck, hit
 
+    @_on_device
     def _trace(self, ray_origin, dirs, scene) -> torch.Tensor:
         blob, S = self.scene_blob(scene)
         D = _as_vector(dirs).to_tensor(self.device)
@@ -374,6 +390,7 @@ class HipRenderer(Renderer):
         self._check_status(ws)
         return res
 
+    @_on_device
     def shade_hits(self, shape, scene, ray_origin, dirs, distance) -> torch.Tensor:
         """NumpyShader.create of ``shape``'s shader for rays hitting ``shape`` at ``distance``
         (shader.py:63-112, rtx_shade_hits); the reflected rays are level 1 of this renderer's
@@ -406,6 +423,7 @@ class HipRenderer(Renderer):
         self._check_status(ws)
         return res
 
+    @_on_device
     def _ray_directions(self, camera: Camera) -> torch.Tensor:
         # a camera-only blob: no shapes needed for ray generation
         pos = (float(camera.position.x), float(camera.position.y), float(camera.position.z))
@@ -422,6 +440,7 @@ class HipRenderer(Renderer):
                 "rtx_ray_directions")
         return out
 
+    @_on_device
     def quantize(self, color, camera: Camera) -> torch.Tensor:
         """Device-side ``(255*clip(c,0,1)).astype(uint8)`` -> [H, W, 3] uint8 (base.py:145-149)."""
         W, H = int(camera.width), int(camera.height)
@@ -442,6 +461,7 @@ class HipRenderer(Renderer):
                 "rtx_quantize_u8")
         return out
 
+    @_on_device
     def assemble_rows(self, tiles: torch.Tensor, width: int, height: int, row_block: int,
                       out: str | None = None) -> torch.Tensor:
         """Frame from gathered row tiles (rtx_assemble_rows, the device un-permute of the

@@ -65,6 +65,17 @@ def _worker(rank, world, port, spec, B, row_block, outdir):
             np.save(os.path.join(outdir, "pipe1.npy"), f1.numpy())
         else:
             assert frame is None and frame_u8 is None and f0 is None and f1 is None
+        # the synchronous path's cached TileGathers: one slot each, at most TILE_GATHER_CACHE kept
+        from python_ray_tracer_amd.distributed import TILE_GATHER_CACHE
+
+        cache = r._tile_gathers
+        assert len(cache) == 2 and all(len(t.send) == 1 for t in cache.values())
+        for w in range(TILE_GATHER_CACHE + 1):
+            small = scenes.build_scene(scenes.readme_spec(8 + w, 5))
+            f = render_frame_distributed(small, r, row_block=row_block)
+            if rank == 0:
+                assert np.array_equal(f.numpy(), O.render(O.scene_from_spec(scenes.readme_spec(8 + w, 5)), B))
+        assert len(cache) == TILE_GATHER_CACHE
 
         # animation driver: frames sharded round-robin, no collective
         class FrameRenderer:
@@ -110,3 +121,23 @@ def test_row_tiled_cpu_baseline_runs():
     assert len(full["times"]) == 2 and full["pixels"] == [48 * 27] * 2
     part = row_tiled.time_row_tiled(spec, 3, 2, frames=2, sub=2, row_block=4)
     assert sum(part["pixels"]) == 48 * 27  # two steps cover the two halves of a 4-way split
+
+
+def test_cpu_baseline_leg_is_bounded(monkeypatch):
+    """bench.py's all-cores CPU leg runs in a child process group with a hard time limit: with a
+    worker stuck before its first frame, the leg returns the 1-core baseline plus
+    ``all_cores_error`` within the limit instead of hanging the bench line; without it, the
+    bounded run returns the row-tiled timing."""
+    import time
+
+    import bench
+
+    spec = scenes.readme_spec(48, 27)
+    single = {"value": 1.5, "unit": "Mpixels/s", "cores": 1, "kind": "port", "sample": "1-core"}
+    ok = bench.cpu_baseline_or_error(spec, 3, 2, 1.0, single, timeout_s=240)
+    assert "all_cores_error" not in ok and ok["cores"] == 2 and ok["single_core"] == single
+    monkeypatch.setenv("ROW_TILED_STALL_RANK", "1")
+    t0 = time.perf_counter()
+    out = bench.cpu_baseline_or_error(spec, 3, 2, 1.0, single, timeout_s=30)
+    assert time.perf_counter() - t0 < 90
+    assert out["value"] == 1.5 and "TimeoutError" in out["all_cores_error"], out

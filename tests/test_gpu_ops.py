@@ -106,3 +106,96 @@ def test_op_argument_checks(env):
     D = torch.zeros(3, 10, dtype=torch.float64, device="cuda")
     with pytest.raises(RuntimeError, match="origins"):
         torch.ops.rt.trace(blob, S, torch.zeros(3, 9, dtype=torch.float64, device="cuda"), D, 3, 0, ws)
+
+
+def test_render_frames_and_shade_hits_ops(env):
+    """rt::render_frames == HipRenderer.render_batch (one launch of F frames) and rt::shade_hits ==
+    HipRenderer.shade_hits (NumpyShader.create on a given batch of hits, shader.py:63-112)."""
+    H = env
+    base = scenes.random_spec(16, 4, 64, 36)
+    frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 8))) for k in range(3)]
+    for B, bl in ((3, 3), (None, -1)):
+        r = H.HipRenderer(max_bounces=B, color_dtype=torch.float32)
+        want = r.render_batch(frames)
+        _, (blobs, F, S, W, Hh) = r._batch_blob(frames)
+        ws = torch.zeros(torch.ops.rt.workspace_bytes(F * W * Hh, bl), dtype=torch.uint8, device="cuda")
+        got = torch.ops.rt.render_frames(blobs, S, W, Hh, bl, 0, ws)
+        assert got.shape == (3, 3, W * Hh) and torch.equal(got, want), B
+        u8 = torch.ops.rt.render_frames(blobs, S, W, Hh, bl, 2, ws)
+        assert u8.shape == (3, Hh, W, 3) and torch.equal(u8, r.render_batch(frames, out="u8")), B
+    spec = scenes.random_spec(16, 3, 80, 45)
+    scene = scenes.build_scene(spec)
+    sc = O.scene_from_spec(spec)
+    d = O.ray_directions(sc.cam, 80, 45)
+    for si, B, bl in ((16, 3, 3), (4, None, -1)):
+        t = O.intersect(sc.spheres[si], *sc.cam, *d)
+        hit = t != O.FARAWAY
+        D = torch.from_numpy(np.stack([c[hit] for c in d])).cuda()
+        T = torch.from_numpy(t[hit]).cuda()
+        org = torch.tensor(sc.cam, dtype=torch.float64, device="cuda")
+        r = H.HipRenderer(max_bounces=B)
+        blob, S = r.scene_blob(scene)
+        ws = torch.zeros(torch.ops.rt.workspace_bytes(D.shape[1], bl), dtype=torch.uint8, device="cuda")
+        got = torch.ops.rt.shade_hits(blob, S, si, org, D, T, bl, 1, ws)
+        assert torch.equal(got, r.shade_hits(scene.shapes[si], scene, H.HipVector3D(*sc.cam), H.HipVector3D(*D), T))
+        want = np.stack(O.create(sc, si, sc.cam, tuple(c[hit] for c in d), t[hit], B))
+        assert np.abs(got.cpu().numpy() - want).max() <= 1e-12, (si, B)
+        with pytest.raises(RuntimeError, match="shape index"):
+            torch.ops.rt.shade_hits(blob, S, S, org, D, T, bl, 1, ws)
+
+
+def test_op_error_channel(env):
+    """A blob whose header disagrees with n_spheres raises before the launch (check=True) or is
+    refused by the kernel and reported by rt::status (check=False); a reflection chain past the
+    unbounded limit raises like HipRenderer's RecursionError, and the sticky flags are cleared, so
+    the next call on the same workspace succeeds (base.py:91-121)."""
+    H = env
+    scene = scenes.build_scene(scenes.readme_spec(32, 18))
+    r = H.HipRenderer(max_bounces=3, color_dtype=torch.float32)
+    blob, S = r.scene_blob(scene)
+    ws = torch.zeros(torch.ops.rt.workspace_bytes(32 * 18, -1), dtype=torch.uint8, device="cuda")
+    with pytest.raises(RuntimeError, match="holds 3 spheres"):
+        torch.ops.rt.render_tile(blob, S - 1, 32, 18, 1, 1, 0, 3, 0, ws)
+    with pytest.raises(RuntimeError, match="holds 3 spheres"):
+        torch.ops.rt.trace(blob, S - 1, torch.zeros(3, dtype=torch.float64, device="cuda"),
+                           torch.ones(3, 5, dtype=torch.float64, device="cuda"), 3, 0, ws)
+    with pytest.raises(RuntimeError, match="bad magic"):
+        torch.ops.rt.render_tile(blob * 0, S, 32, 18, 1, 1, 0, 3, 0, ws)
+    torch.ops.rt.render_tile(blob, S - 1, 32, 18, 1, 1, 0, 3, 0, ws, check=False)  # the kernel refuses it
+    assert torch.ops.rt.status(ws) == 4  # RTX_ST_BAD_SCENE, read and cleared
+    assert torch.ops.rt.status(ws) == 0
+    good = torch.ops.rt.render_tile(blob, S, 32, 18, 1, 1, 0, 3, 0, ws)
+    assert torch.equal(good, r.render(scene).data)
+    # the trapped-ray scene of test_gpu_parity.test_unbounded_recursion_limit
+    spec = scenes.readme_spec(8, 8)
+    spec["spheres"] = [{"center": [0, 0.2, -2], "radius": -5.0,
+                        "shader": {"reflection_gain": 1, "specular_gain": 1.0, "specular_roughness": 0.5,
+                                   "iridescence_gain": 0, "diffuse_gain": 0.5,
+                                   "texture": {"kind": "const", "color": [1, 1, 1]}}}]
+    spec["lights"][0]["position"] = [0, 0.2, -2]
+    trap = scenes.build_scene(spec)
+    tb, tS = r.scene_blob(trap)
+    with pytest.raises(RuntimeError, match="maximum recursion depth"):
+        torch.ops.rt.render_tile(tb, tS, 8, 8, 1, 1, 0, -1, 0, ws)
+    assert torch.ops.rt.status(ws) == 0  # cleared by the raising call
+    torch.ops.rt.render_tile(tb, tS, 8, 8, 1, 1, 0, -1, 0, ws, check=False)
+    assert torch.ops.rt.status(ws) & 1  # RTX_ST_STACK_OVERFLOW
+    ru = H.HipRenderer(color_dtype=torch.float32)
+    assert torch.equal(torch.ops.rt.render_tile(blob, S, 32, 18, 1, 1, 0, -1, 0, ws), ru.render(scene).data)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_ops_follow_the_input_device(env):
+    """Every op runs under a device guard of its input: tensors on cuda:1 while cuda:0 is current
+    give what the same call gives with cuda:1 current."""
+    H = env
+    scene = scenes.build_scene(scenes.random_spec(40, 1, 64, 40))
+    torch.cuda.set_device(1)
+    r1 = H.HipRenderer(max_bounces=3, color_dtype=torch.float32, device="cuda:1")
+    want = r1.render(scene).data.cpu()
+    blob, S = r1.scene_blob(scene)
+    ws = torch.zeros(torch.ops.rt.workspace_bytes(64 * 40, 3), dtype=torch.uint8, device="cuda:1")
+    torch.cuda.set_device(0)
+    got = torch.ops.rt.render_tile(blob, S, 64, 40, 1, 1, 0, 3, 0, ws)
+    assert got.device == torch.device("cuda:1") and torch.equal(got.cpu(), want)
+    assert torch.equal(r1.render(scene).data.cpu(), want)  # HipRenderer's own guard

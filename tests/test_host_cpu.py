@@ -2,7 +2,10 @@
 No compute call reaches the GPU here."""
 
 import ctypes
+import os
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -302,6 +305,55 @@ def test_torch_ops_registered_and_checked_on_host():
         torch.ops.rt.quantize_u8(torch.zeros(3, 4))
     with pytest.raises(RuntimeError):
         torch.ops.rt.assemble_rows(torch.zeros(2, 64, dtype=torch.uint8), 4, 4, 1, 2)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.render_frames(torch.zeros(2, 200, dtype=torch.float64), 3, 8, 8, 3, 0, ws)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.shade_hits(blob, 3, 0, torch.zeros(3, dtype=torch.float64), torch.zeros(3, 5, dtype=torch.float64),
+                                torch.zeros(5, dtype=torch.float64), 3, 0, ws)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.status(ws)
+
+
+def test_torch_ops_schema_and_fake_kernels():
+    """The render ops declare their workspace and stats as mutated (Tensor(a!), Tensor(b!)?) and
+    carry a check flag; every op has a Meta kernel returning the output a GPU call returns, so the
+    surface traces under FakeTensor (torch.compile) without a GPU."""
+    import python_ray_tracer_amd.ops  # noqa: F401
+
+    for name in ("render_tile", "render_frames", "trace", "shade_hits"):
+        s = str(getattr(torch.ops.rt, name).default._schema)
+        assert "Tensor(a!) workspace" in s and "Tensor(b!)? stats=None" in s and "bool check=True" in s, s
+    meta = {"device": "meta"}
+    blob = torch.empty(64 + 3 * 32, dtype=torch.float64, **meta)
+    ws = torch.empty(1 << 20, dtype=torch.uint8, **meta)
+    st = torch.empty(264, dtype=torch.int64, **meta)
+    assert torch.ops.rt.render_tile(blob, 3, 20, 17, 1, 1, 0, 3, 0, ws, st).shape == (3, 340)
+    out = torch.ops.rt.render_tile(blob, 3, 20, 17, 4, 3, 1, 3, 2, ws)  # rows 4-7 and 16: 5 rows
+    assert out.shape == (5, 20, 3) and out.dtype == torch.uint8
+    assert torch.ops.rt.render_tile(blob, 3, 20, 17, 1, 1, 0, 3, 1, ws).dtype == torch.float64
+    frames = torch.empty(4, 160, dtype=torch.float64, **meta)
+    assert torch.ops.rt.render_frames(frames, 3, 20, 17, 3, 2, ws).shape == (4, 17, 20, 3)
+    assert torch.ops.rt.render_frames(frames, 3, 20, 17, 3, 0, ws).shape == (4, 3, 340)
+    d = torch.empty(3, 11, dtype=torch.float64, **meta)
+    o = torch.empty(3, dtype=torch.float64, **meta)
+    assert torch.ops.rt.trace(blob, 3, o, d, -1, 1, ws).shape == (3, 11)
+    t = torch.empty(11, dtype=torch.float64, **meta)
+    assert torch.ops.rt.shade_hits(blob, 3, 1, o, d, t, 3, 0, ws).dtype == torch.float32
+    assert torch.ops.rt.intersect(blob[:8], o, d).shape == (11,)
+    assert torch.ops.rt.quantize_u8(d).shape == (11, 3)
+    assert torch.ops.rt.assemble_rows(torch.empty(2, 64, dtype=torch.uint8, **meta), 4, 4, 1, 2).shape == (4, 4, 3)
+
+
+def test_ops_refuse_a_variant_library():
+    """RTX_HIP_LIB (an A/B variant of librtx_hip.so for HipRenderer) cannot be mixed with the ops,
+    which link the in-tree library by $ORIGIN: importing the ops then raises ImportError."""
+    code = ("import os, sys; sys.path.insert(0, os.getcwd())\n"
+            "try:\n    import python_ray_tracer_amd.ops\nexcept ImportError as e:\n"
+            "    print('refused:', e); sys.exit(0)\nsys.exit(3)\n")
+    env = dict(os.environ, RTX_HIP_LIB=str(REPO / "python_ray_tracer_amd" / "variant_librtx_hip.so"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(REPO), env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "RTX_HIP_LIB" in r.stdout, r.stdout + r.stderr
 
 
 def test_pack_image_texture():
