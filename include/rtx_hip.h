@@ -83,9 +83,13 @@ enum {
   RTX_H_NALWAYS = 34,/* leading entries of the culled geometry list tested by every ray (huge spheres) */
   RTX_H_NODES = 35,  /* word offset of the node array (RTX_NODE_WORDS each)                 */
   RTX_H_CGEO = 36,   /* word offset of the culled geometry list (S records, RTX_GEOM_WORDS)  */
-  RTX_H_TAME = 37    /* 1: every coordinate (centres, camera) and radius below 2^60 in magnitude, so
+  RTX_H_TAME = 37,   /* 1: every coordinate (centres, camera) and radius below 2^60 in magnitude, so
                         the fast kernel may use the half-b sphere test (rtx_kernels.hip SphTest); 0: the
                         reference expressions everywhere */
+  RTX_H_MAT0 = 38    /* rtx_shade_hits only: word offset of a material record (RTX_MAT_WORDS) that
+                        replaces the shape's own at level 0 — NumpyShader.create called on another
+                        shape's shader (shader.py:63-112 reads self.* for the hit, and traces the
+                        reflections through the unchanged scene, :152); 0 = none */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 
@@ -239,8 +243,10 @@ int rtx_trace_rays(const double* scene, int n_spheres, const double* origins, in
  * colour of n rays that hit sphere `shape` at distances t[n] — P = O + D*t, shadow, diffuse, dome,
  * specular, iridescence, and the reflection recursion through raytrace_scene up to max_bounces
  * (the reflected rays are level 1; -1 = unbounded). The shape is taken as hit whether or not it is
- * the nearest, as create shades what it is handed. Same origins/dirs layout as rtx_trace_rays;
- * out_kind colour or u8; workspace rtx_workspace_bytes(n, max_bounces). */
+ * the nearest, as create shades what it is handed. A blob whose RTX_H_MAT0 word is set shades the
+ * level-0 hits with that material record instead of the shape's own (create on another shape's
+ * shader). Same origins/dirs layout as rtx_trace_rays; out_kind colour or u8; workspace
+ * rtx_workspace_bytes(n, max_bounces). */
 int rtx_shade_hits(const double* scene, int n_spheres, int shape, const double* origins, int64_t origin_stride,
                    const double* dirs, const double* t, int64_t n, int max_bounces, void* out, int out_kind,
                    void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);

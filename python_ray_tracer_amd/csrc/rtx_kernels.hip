@@ -958,12 +958,13 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 // assembly (hit_color) and the reflection recursion (driven by the caller).
 // geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
 // same table (LDS copy or global).
+// mat: a material record replacing sphere h's own (Shader.create on another shape's shader), or null.
 template <bool IMG = false, typename T, typename G, typename Wk>
 __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* tab, int nsph, int h, double ox,
                                       double oy, double oz, double dx, double dy, double dz, double t, Hit& s,
-                                      double tame, Wk& wk) {
+                                      double tame, Wk& wk, const T* mat = nullptr) {
   const T* gh = tab + h * RTX_GEOM_WORDS;
-  const T* mh = tab + nsph * RTX_GEOM_WORDS + h * RTX_MAT_WORDS;
+  const T* mh = mat ? mat : tab + nsph * RTX_GEOM_WORDS + h * RTX_MAT_WORDS;
   const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73
   const double inv_r = gh[RTX_G_INVR];
   const double nx = (px - gh[RTX_G_CX]) * inv_r;  // :74 (not renormalised)
@@ -1234,6 +1235,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (p.mode == 3) {  // NumpyShader.create: the hit is given (shader.py:63-73)
       tmin = p.hit_t[i];
       hit = p.hit_shape;
+      // create on another shape's shader (RTX_H_MAT0): the general kernel shades this level-0 hit
+      // with that material, deferred like a tie
+      tie = sc[RTX_H_MAT0] != 0.0;
     } else if (sc[RTX_H_NNODES] != 0.0) {
       if (cam0) {
         nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
@@ -1276,7 +1280,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       deferred = true;
       rays_through = kb + k;
       hits_through = kb + k - 1;
-      if (st) stat_add(st, RTX_S_TIES, 1);
+      if (st && !(p.mode == 3 && kb + k == 0)) stat_add(st, RTX_S_TIES, 1);  // (not the RTX_H_MAT0 deferral)
       break;
     }
     Hit s;
@@ -1542,6 +1546,8 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
   const double* mtab = tab + p.nsph * RTX_GEOM_WORDS;
   const int nsph = p.nsph;
   const int B = p.max_bounces;  // < 0: unbounded (bounded by the stack depth)
+  // Shader.create on another shape's shader: level 0 shades with that material (RTX_H_MAT0)
+  const double* mat0 = (h_given >= 0 && sc[RTX_H_MAT0] != 0.0) ? p.scene + (int64_t)sc[RTX_H_MAT0] : nullptr;
   unsigned long long* st = p.stats;
 
   int d = 0;
@@ -1620,8 +1626,8 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       const int key = (int)S.at(d, F_KEY);
       const int ph = key_hit(key);
       double xr, xg, xb;
-      hit_color<true>(mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI), key_tex(key), true, true,
-                S.at(d, F_SPEC), S.at(d, F_VA), rr, rg, rb, xr, xg, xb);
+      hit_color<true>((d == 0 && mat0) ? mat0 : mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI),
+                      key_tex(key), true, true, S.at(d, F_SPEC), S.at(d, F_VA), rr, rg, rb, xr, xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
       S.at(d, F_AB) = S.at(d, F_AB) + xb;
@@ -1632,7 +1638,8 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     if (st && d < RTX_S_LEVELS && d > hits_through) stat_add(st, RTX_S_HITS + d, 1);
     Hit s;
     Work<false> nowk;
-    shade<true>(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, __builtin_nan(""), nowk);
+    shade<true>(sc, geo, tab, nsph, h, ox, oy, oz, dx, dy, dz, tmin, s, __builtin_nan(""), nowk,
+                d == 0 ? mat0 : nullptr);
     const bool weighted = s.lit && s.g != 0.0;
     bool descend = weighted && (B < 0 || d < B);
     if (descend && d + 1 >= p.stack_levels) {  // deeper than the stack: RecursionError on the host
@@ -1641,8 +1648,8 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     }
     if (!descend) {
       double xr, xg, xb;
-      hit_color<true>(mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec, s.va, 0.0, 0.0, 0.0, xr,
-                xg, xb);
+      hit_color<true>((d == 0 && mat0) ? mat0 : mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted,
+                      s.spec, s.va, 0.0, 0.0, 0.0, xr, xg, xb);
       S.at(d, F_AR) = S.at(d, F_AR) + xr;
       S.at(d, F_AG) = S.at(d, F_AG) + xg;
       S.at(d, F_AB) = S.at(d, F_AB) + xb;

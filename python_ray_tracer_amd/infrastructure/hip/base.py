@@ -391,14 +391,18 @@ class HipRenderer(Renderer):
         return res
 
     @_on_device
-    def shade_hits(self, shape, scene, ray_origin, dirs, distance) -> torch.Tensor:
-        """NumpyShader.create of ``shape``'s shader for rays hitting ``shape`` at ``distance``
-        (shader.py:63-112, rtx_shade_hits); the reflected rays are level 1 of this renderer's
-        bounce cap. Returns [3, n] colour."""
+    def shade_hits(self, shape, scene, ray_origin, dirs, distance, shader=None) -> torch.Tensor:
+        """NumpyShader.create of ``shader`` (default: ``shape``'s own) for rays hitting ``shape`` at
+        ``distance`` (shader.py:63-112, rtx_shade_hits); the reflected rays are level 1 of this
+        renderer's bounce cap and see the scene unchanged (another shape's shader shades only the
+        level-0 hits, RTX_H_MAT0). Returns [3, n] colour."""
         si = next((k for k, s in enumerate(scene.shapes) if s is shape), None)
         if si is None:  # scene.shapes.index(shape) in _calculate_shadow (shader.py:126)
             raise ValueError("shape is not in scene.shapes")
-        blob, S = self.scene_blob(scene)
+        if shader is None or shader is getattr(shape, "shader", None):
+            blob, S = self.scene_blob(scene)
+        else:
+            blob, S = self._override_blob(scene, si, shape, shader)
         D = _as_vector(dirs).to_tensor(self.device)
         if D.dim() != 2:
             D = D.reshape(3, 1)
@@ -422,6 +426,25 @@ class HipRenderer(Renderer):
                 "rtx_shade_hits")
         self._check_status(ws)
         return res
+
+    def _override_blob(self, scene, si, shape, shader):
+        """The scene blob with a level-0 material record for ``shader`` (scene_pack.pack_override),
+        cached by content like scene_blob."""
+        import types
+
+        from .scene_pack import _shape_fields, pack_override
+
+        pos = getattr(shape, "position", None) or getattr(shape, "center", None)
+        key = ("mat0", scene_key(scene), si,
+               _shape_fields(types.SimpleNamespace(position=pos, radius=shape.radius, shader=shader)))
+        hit = self._scene_cache.get(key)
+        if hit is None:
+            blob = pack_override(scene, shape, shader)
+            hit = (torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True), int(blob[L.H_NSPH]))
+            if len(self._scene_cache) >= 16:
+                self._scene_cache.pop(next(iter(self._scene_cache)))
+            self._scene_cache[key] = hit
+        return hit
 
     @_on_device
     def _ray_directions(self, camera: Camera) -> torch.Tensor:

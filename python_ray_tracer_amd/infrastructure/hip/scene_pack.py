@@ -150,38 +150,13 @@ def _pack_static(static: tuple) -> np.ndarray:
     h[L.H_NDOME] = len(domes)
 
     geo_rows, mat_rows = [], []
-    for (cx, cy, cz), radius, tex, g, dg, rough, ior, ig, tfw, tft, tfior, refl in spheres:
+    for sp in spheres:
+        (cx, cy, cz), radius = sp[0], sp[1]
         cc = (cx * cx + cy * cy) + cz * cz  # abs(self.position), shape.py:35
         rr = radius * radius  # shape.py:36
         # G_C0 (camera-dependent) is filled by _apply_camera
         geo_rows.append((cx, cy, cz, cc, rr, 1.0 / radius, 0.0, 0.0))  # 1/r: shader.py:74
-        m = [0.0] * L.MAT_WORDS
-        m[L.M_G] = g
-        m[L.M_DG] = dg
-        if tex[0] == L.TEX_IMAGE:  # the texel table's offset is set below, once the blob is laid out
-            m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = L.TEX_IMAGE, 0.0, tex[2], tex[3]
-        else:
-            m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = tex
-        # _calculate_physical_specular constants (shader.py:290-301), same Python expressions
-        alpha = rough**2
-        F0 = ((ior - 1) / (ior + 1)) ** 2
-        m[L.M_A2] = alpha**2
-        m[L.M_A2M1] = alpha**2 - 1
-        m[L.M_1MA2] = 1 - alpha**2
-        m[L.M_F0] = F0
-        m[L.M_1MF0] = 1 - F0
-        # _calculate_physical_iridescence constants (shader.py:208-232)
-        hue_shift = (tfior - 1.0) / 2.0
-        m[L.M_IG] = ig
-        m[L.M_TFW] = tfw
-        m[L.M_TFT] = tft
-        m[L.M_HS] = hue_shift
-        m[L.M_1MHS] = 1.0 - hue_shift
-        m[L.M_ROUGH] = rough
-        m[L.M_REFL] = refl
-        m[L.M_IOR] = ior
-        m[L.M_TFIOR] = tfior
-        mat_rows.append(m)
+        mat_rows.append(_material_row(sp))
     geo = blob[L.HDR_WORDS: L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
     geo[:] = np.asarray(geo_rows, dtype=np.float64)
     blob[L.HDR_WORDS + S * L.GEOM_WORDS:] = np.asarray(mat_rows, dtype=np.float64).ravel()
@@ -204,6 +179,62 @@ def _pack_static(static: tuple) -> np.ndarray:
         blob = np.concatenate([blob] + [t.ravel() for t in textures])
     blob.setflags(write=False)
     return blob
+
+
+def _material_row(fields) -> list:
+    """The RTX_MAT_WORDS material record of one sphere's _shape_fields (an image texture's texel
+    table offset, RTX_M_TR, is left 0 for the caller to set once the blob is laid out)."""
+    _, _, tex, g, dg, rough, ior, ig, tfw, tft, tfior, refl = fields
+    m = [0.0] * L.MAT_WORDS
+    m[L.M_G] = g
+    m[L.M_DG] = dg
+    if tex[0] == L.TEX_IMAGE:
+        m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = L.TEX_IMAGE, 0.0, tex[2], tex[3]
+    else:
+        m[L.M_TEX], m[L.M_TR], m[L.M_TG], m[L.M_TB] = tex
+    # _calculate_physical_specular constants (shader.py:290-301), same Python expressions
+    alpha = rough**2
+    F0 = ((ior - 1) / (ior + 1)) ** 2
+    m[L.M_A2] = alpha**2
+    m[L.M_A2M1] = alpha**2 - 1
+    m[L.M_1MA2] = 1 - alpha**2
+    m[L.M_F0] = F0
+    m[L.M_1MF0] = 1 - F0
+    # _calculate_physical_iridescence constants (shader.py:208-232)
+    hue_shift = (tfior - 1.0) / 2.0
+    m[L.M_IG] = ig
+    m[L.M_TFW] = tfw
+    m[L.M_TFT] = tft
+    m[L.M_HS] = hue_shift
+    m[L.M_1MHS] = 1.0 - hue_shift
+    m[L.M_ROUGH] = rough
+    m[L.M_REFL] = refl
+    m[L.M_IOR] = ior
+    m[L.M_TFIOR] = tfior
+    return m
+
+
+def pack_override(scene, shape, shader) -> np.ndarray:
+    """The blob of ``scene`` plus a level-0 material record for ``shader`` (RTX_H_MAT0):
+    NumpyShader.create called on a shader that is not ``shape``'s own shades the hits with the
+    shader's parameters on the shape's geometry (shader.py:73-112 reads ``self.*``), and traces the
+    reflections through the unchanged scene (shader.py:152). An image texture's texels are appended
+    after the record."""
+    import types
+
+    static, camera = scene_key(scene)
+    pos = getattr(shape, "position", None) or getattr(shape, "center", None)
+    fields = _shape_fields(types.SimpleNamespace(position=pos, radius=shape.radius, shader=shader))
+    m = _material_row(fields)
+    blob = pack_key(static, camera)
+    off = blob.size
+    parts = [blob, np.asarray(m, dtype=np.float64)]
+    if fields[2][0] == L.TEX_IMAGE:
+        parts[1][L.M_TR] = off + L.MAT_WORDS
+        parts.append(fields[2][1].texels.ravel())
+    out = np.concatenate(parts)
+    out[L.H_MAT0] = off
+    return out
 
 
 def _apply_camera(blob: np.ndarray, cpos, W: int, H: int) -> None:
@@ -247,6 +278,12 @@ def is_tame(geo: np.ndarray, cpos) -> bool:
 BVH_MIN_SPHERES = 8
 BVH_LEAF = 8
 HUGE_RADIUS = 100.0
+# Split criterion (surface-area heuristic): a node of n spheres is split when
+#   node_cost * 2 + (A_left * n_left + A_right * n_right) / A < n   (costs in sphere tests),
+# i.e. when testing the two child boxes plus the expected sphere tests behind them is cheaper than
+# testing the n spheres; nodes above BVH_LEAF spheres always split. None: split every node above
+# BVH_LEAF (round 2's build).
+BVH_NODE_COST = None
 
 
 def _box(centers: np.ndarray, radii: np.ndarray):
@@ -296,15 +333,25 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
         R = R * (1 + 1e-12) + 1e-12
         cc = (float(np.sqrt((c ** 2).sum())) + R) ** 2
         node = [lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], 0, 0, 0, 2e-7 * (3.0 * cc + R * R + 1.0), 0.0, 0.0]
-        if len(idx) <= BVH_LEAF:
+        split = None
+        if len(idx) > 1:
+            left, right = _sah_split(idx, centers, radii)
+            if len(idx) > BVH_LEAF:
+                split = (left, right)
+            elif BVH_NODE_COST is not None:
+                a = _area(lo, hi)
+                al = _area(*_box(centers[left], radii[left]))
+                ar = _area(*_box(centers[right], radii[right]))
+                if a > 0 and 2 * BVH_NODE_COST + (al * len(left) + ar * len(right)) / a < len(idx):
+                    split = (left, right)
+        if split is None:
             node[L.N_FIRST] = len(order)
             node[L.N_COUNT] = len(idx)
             order.extend(sorted(idx))
         else:
-            left, right = _sah_split(idx, centers, radii)
             nodes[me] = node
-            rec(left)
-            rec(right)
+            rec(split[0])
+            rec(split[1])
         node[L.N_SKIP] = len(nodes)
         nodes[me] = node
 

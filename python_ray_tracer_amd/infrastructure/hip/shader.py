@@ -95,19 +95,12 @@ class HipShader(Shader):
         iridescence and the reflection recursion (shader.py:143-161), one ``rtx_shade_hits``
         launch. ``ray_tracer``: the HipRenderer whose bounce cap the reflections follow (the
         reference re-enters ``ray_tracer.raytrace_scene``); any other value uses an unbounded
-        HipRenderer, as the reference NumpyRenderer recursion is. Returns a HipRGBColor over a
-        [3, n] device tensor."""
-        import copy
-
-        from python_ray_tracer_amd.domain import Scene3D
-
+        HipRenderer, as the reference NumpyRenderer recursion is. Called on another shape's
+        shader, the hits are shaded with this shader's parameters on ``shape``'s geometry and the
+        reflections are traced through the unchanged scene, as in the reference (shader.py:73-112,
+        :152). Returns a HipRGBColor over a [3, n] device tensor."""
         from .base import HipRenderer, HipRGBColor
 
         r = ray_tracer if isinstance(ray_tracer, HipRenderer) else HipRenderer()
-        if getattr(shape, "shader", None) is not self:
-            # the reference shades with this shader's parameters on that shape's geometry
-            proxy = copy.copy(shape)
-            proxy.shader = self
-            shapes = [proxy if s is shape else s for s in scene.shapes]
-            scene, shape = Scene3D(shapes, scene.lights, scene.camera), proxy
-        return HipRGBColor.from_tensor(r.shade_hits(shape, scene, ray_origin, normalized_ray_direction, distance))
+        return HipRGBColor.from_tensor(r.shade_hits(shape, scene, ray_origin, normalized_ray_direction, distance,
+                                                    shader=self))

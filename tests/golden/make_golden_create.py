@@ -37,9 +37,14 @@ def main():
         "main_s1_B2": (S.main_spec(40, 24), 1, 2),
         "rand16_s9_B4": (S.random_spec(16, 0, 96, 54), 9, 4),
         "rand16_s12_Binf": (S.random_spec(16, 0, 96, 54), 12, None),
+        # create called on ANOTHER shape's shader: the hit is shaded with that shader's parameters,
+        # the reflections are traced through the unchanged scene (shader.py:73-112, :152)
+        "rand16_s9_shader3_B3": (S.random_spec(16, 0, 96, 54), 9, 3, 3),
+        "readme_ground_shader0_Binf": (S.readme_spec(48, 27), 2, None, 0),
+        "rand16_s12_shader16_B2": (S.random_spec(16, 0, 96, 54), 12, 2, 16),
     }
     arrays, meta = {}, {"note": "reference NumpyShader.create on the rays that hit the shape", "cases": {}}
-    for name, (spec, si, B) in cases.items():
+    for name, (spec, si, B, *other) in cases.items():
         scene = G.ref_scene(spec)
         rend = G.CappedRenderer(B)
         dirs = rend.get_ray_directions(scene.camera)
@@ -49,14 +54,16 @@ def main():
         D = V(dirs.x[hit], dirs.y[hit], dirs.z[hit])
         O = scene.camera.position
         rend.depth = 1  # inside level 0's raytrace_scene: the reflection is level 1
-        col = shape.shader.create(shape, scene, O, D, t[hit], rend)
+        shader = scene.shapes[other[0]].shader if other else shape.shader
+        col = shader.create(shape, scene, O, D, t[hit], rend)
         n = int(hit.sum())
         out = np.stack([np.broadcast_to(np.asarray(c, dtype=np.float64), (n,)) for c in col.components()])
         arrays[f"{name}_dirs"] = np.stack([D.x, D.y, D.z])
         arrays[f"{name}_t"] = t[hit]
         arrays[f"{name}_rgb"] = out
         meta["cases"][name] = {"spec": spec, "shape": si, "max_bounces": B, "n": n,
-                               "origin": [float(O.x), float(O.y), float(O.z)]}
+                               "origin": [float(O.x), float(O.y), float(O.z)],
+                               "shader_of": other[0] if other else si}
         print(name, n, "rays")
     np.savez_compressed(HERE / "create_kat.npz", **arrays)
     (HERE / "create_kat.json").write_text(json.dumps(meta, indent=1))

@@ -448,9 +448,10 @@ def test_shader_create_matches_reference(hip):
     for name, c in meta["cases"].items():
         scene = scenes.build_scene(c["spec"])
         shape = scene.shapes[c["shape"]]
+        shader = scene.shapes[c.get("shader_of", c["shape"])].shader  # the shape's own, or another's
         r = hip.HipRenderer(max_bounces=c["max_bounces"])
-        col = shape.shader.create(shape, scene, hip.HipVector3D(*c["origin"]), hip.HipVector3D(*z[name + "_dirs"]),
-                                  z[name + "_t"], r)
+        col = shader.create(shape, scene, hip.HipVector3D(*c["origin"]), hip.HipVector3D(*z[name + "_dirs"]),
+                            z[name + "_t"], r)
         assert np.abs(col.data.cpu().numpy() - z[name + "_rgb"]).max() <= ATOL, name
     # a bigger batch with per-ray origins against the oracle; and another shape's shader
     spec = scenes.random_spec(16, 3, 80, 45)
@@ -464,12 +465,8 @@ def test_shader_create_matches_reference(hip):
         r = hip.HipRenderer(max_bounces=B)
         shader = scene.shapes[si].shader if foreign is None else scene.shapes[foreign].shader
         got = shader.create(scene.shapes[si], scene, hip.HipVector3D(*sc.cam), hip.HipVector3D(*dd), t[hit], r)
-        osc = sc
-        if foreign is not None:
-            ospec = json.loads(json.dumps(spec))
-            ospec["spheres"][si]["shader"] = spec["spheres"][foreign]["shader"]
-            osc = O.scene_from_spec(ospec)
-        want = np.stack(O.create(osc, si, sc.cam, dd, t[hit], B))
+        mat = None if foreign is None else sc.spheres[foreign]  # level 0 only; reflections see the scene
+        want = np.stack(O.create(sc, si, sc.cam, dd, t[hit], B, material=mat))
         assert np.abs(got.data.cpu().numpy() - want).max() <= ATOL, (si, B, foreign)
     with pytest.raises(ValueError):
         scene.shapes[0].shader.create(hip.HipSphere(hip.HipVector3D(0, 0, 0), 1.0, None), scene,

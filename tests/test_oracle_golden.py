@@ -106,8 +106,10 @@ def test_oracle_create_matches_reference_fixtures():
     meta = json.loads((GOLDEN / "create_kat.json").read_text())
     for name, c in meta["cases"].items():
         sc = O.scene_from_spec(c["spec"])
+        other = c.get("shader_of", c["shape"])
+        mat = sc.spheres[other] if other != c["shape"] else None  # create on another shape's shader
         got = np.stack(O.create(sc, c["shape"], tuple(c["origin"]), tuple(z[name + "_dirs"]), z[name + "_t"],
-                                c["max_bounces"]))
+                                c["max_bounces"], material=mat))
         assert np.abs(got - z[name + "_rgb"]).max() <= 1e-12, name
 
 
