@@ -66,6 +66,7 @@ constexpr int kLevelsLdsSlots = 3;   // levels kept in LDS; deeper ones (B = 4) 
 constexpr int kB5Slots = 2;          // LDS level slots of the B >= 5 kernels (the others in a register shift)
 constexpr int kB5Waves = 4;          // their waves/SIMD
 constexpr int kLvWaves = 5;          // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
+constexpr int kLvWavesSmall = 5;     // ... and of their TREE = false instantiations (scenes below kTreeMinSpheres)
 constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
 constexpr int kDeepWaves = 3;        // waves/SIMD of the DEEP instantiation (records + continuation need registers)
 constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
@@ -110,6 +111,9 @@ __host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)lev
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
+// scenes of fewer spheres never carry a culling tree (scene_pack.BVH_MIN_SPHERES): the fast kernel's
+// TREE = false instantiations serve them
+constexpr int kTreeMinSpheres = 8;
 constexpr size_t kLdsBytesPerCu = 160 * 1024;  // gfx950
 
 // Wave-uniform loads through the scalar cache: the constant address space makes hipcc emit s_load
@@ -959,7 +963,8 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 // geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
 // same table (LDS copy or global).
 // mat: a material record replacing sphere h's own (Shader.create on another shape's shader), or null.
-template <bool IMG = false, typename T, typename G, typename Wk>
+// TREE = false: the scene has no culling tree (fewer than kTreeMinSpheres spheres), compiled out.
+template <bool IMG = false, bool TREE = true, typename T, typename G, typename Wk>
 __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* tab, int nsph, int h, double ox,
                                       double oy, double oz, double dx, double dy, double dz, double t, Hit& s,
                                       double tame, Wk& wk, const T* mat = nullptr) {
@@ -988,7 +993,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
   const int h0 = __builtin_amdgcn_readfirstlane(h);
   const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
-  const bool culled = sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
+  const bool culled = TREE && sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
   if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
   const int nshadow = culled ? 0 : nsph - (hs < nsph);
   int j = 0;
@@ -1165,7 +1170,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // overlaps the LDS staging of the scene table. DEEP (caps above 8 or none): chains still alive
 // after B levels are deferred with a resume record, and the continuation mode exists; the capped
 // instantiations compile none of it.
-template <int B, bool LDS, bool DEEP, bool LVL, bool STATS>
+template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   const cdouble* sc = (const cdouble*)p.scene;
@@ -1238,7 +1243,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       // create on another shape's shader (RTX_H_MAT0): the general kernel shades this level-0 hit
       // with that material, deferred like a tie
       tie = sc[RTX_H_MAT0] != 0.0;
-    } else if (sc[RTX_H_NNODES] != 0.0) {
+    } else if (TREE && sc[RTX_H_NNODES] != 0.0) {
       if (cam0) {
         nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else {
@@ -1285,9 +1290,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     Hit s;
     if constexpr (LDS) {
-      shade(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
+      shade<false, TREE>(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
     } else {
-      shade(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
+      shade<false, TREE>(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
     }
     if (s.tk < 0) {  // an image-textured sphere: so is this one (the texel lookup stays out of here)
       deferred = true;
@@ -1375,7 +1380,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_add(st, RTX_S_RAYS + kb + k + 1, 1);
       stat_wave(st, RTX_S_WTRACE + kb + k + 1);
     }
-    if (sc[RTX_H_NNODES] != 0.0) {
+    if (TREE && sc[RTX_H_NNODES] != 0.0) {
       nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     } else if constexpr (LDS) {
       nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
@@ -1441,8 +1446,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   write_out(p, i, cr, cg, cb);
 }
 
-template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false>
-__global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : kLvWaves) : kFastWavesPerSimd)) void k_render_fast(Params p0) {
+template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, bool TREE = true>
+__global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TREE ? kLvWaves : kLvWavesSmall)
+                                                                   : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
@@ -1464,12 +1470,12 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
       for (int64_t t = blockIdx.x; t * kFastBlock < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP, LVL, STATS>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+        fast_tile<B, LDS, DEEP, LVL, STATS, TREE>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
     }
   }
-  if (p.n_fetch > 0) {
+  if (TREE && p.n_fetch > 0) {  // (persistent launches are for scenes of kPersistMinSpheres and more)
     // Persistent waves fetching kWaveW x kWaveH tiles, bottom-up (longest work first, as below).
     // Counter c (of n_fetch) hands out tiles c, c + n_fetch, ... . Waves are numbered XCD-major
     // (pw; block b runs on XCD b % 8) and wave pw uses counter pw % n_fetch, so every counter's
@@ -1495,7 +1501,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
     while (k < tiles_c) {
       const int t = c + k * nc;
       const int row = t / p.n_tiles_x;
-      fast_tile<B, LDS, DEEP, LVL, STATS>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
+      fast_tile<B, LDS, DEEP, LVL, STATS, TREE>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
       if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
@@ -1509,7 +1515,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
   // spheres, whose pixels run long bounce chains, while sky rows finish at level 0 and so fill the
   // end of the grid (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on
   // the order.
-  fast_tile<B, LDS, DEEP, LVL, STATS>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
+  fast_tile<B, LDS, DEEP, LVL, STATS, TREE>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1954,10 +1960,17 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
   return dim3((unsigned)blocks);
 }
 
-// STATS: the instantiation with the per-level and executed-work counters (stats buffer given)
+// STATS: the instantiation with the per-level and executed-work counters (stats buffer given).
+// Scenes below kTreeMinSpheres carry no culling tree (scene_pack.BVH_MIN_SPHERES) and never take the
+// persistent launch: their instantiations (TREE = false) compile neither (A/B in DESIGN.md §4).
 template <int B, bool DEEP, bool LVL, bool STATS>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
+  if (p.nsph < kTreeMinSpheres && p.n_fetch == 0) {
+    hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, false>), grid, dim3(kFastBlock), (uint32_t)lds,
+                          s, prof_event(0), prof_event(1), 0u, p);
+    return;
+  }
   if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL, STATS>, lds, p);
   hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS>), grid, dim3(kFastBlock), (uint32_t)lds, s,
                         prof_event(0), prof_event(1), 0u, p);

@@ -75,6 +75,45 @@ def source_functions(path: Path):
     return out
 
 
+def _chain(comment: str):
+    """Source lines of a .loc comment's inline chain, innermost first (file rtx_kernels.hip)."""
+    return [int(m) for m in re.findall(r"rtx_kernels\.hip:(\d+):\d+", comment)]
+
+
+def stages(asm_path: str, symbol: str, root_line: int, outer: tuple, inner: tuple | None = None):
+    """Per-stage static budget of the code inlined at kernel line ``root_line`` (one fast_tile call
+    site): an instruction's stage is the line of its inline chain that lies in ``outer`` (first,
+    last source line: the function whose call sites name the stages, e.g. fast_tile); inside
+    ``inner`` (e.g. shade) it is refined by the line there."""
+    out = defaultdict(Counter)
+    inside = False
+    chain = []
+    with open(asm_path) as f:
+        for raw in f:
+            if not inside:
+                if raw.startswith(symbol + ":"):
+                    inside = True
+                continue
+            s = raw.strip()
+            if s.startswith(".Lfunc_end") or s.startswith("; -- End function"):
+                break
+            if s.startswith(".loc"):
+                chain = _chain(s)
+                continue
+            if not s or s.startswith((".", ";", "//")) or s.endswith(":"):
+                continue
+            if not chain or chain[-1] != root_line:
+                continue
+            st = next((ln for ln in chain if outer[0] <= ln <= outer[1]), None)
+            key = f"L{st}" if st is not None else "kernel"
+            if inner is not None:
+                sub = next((ln for ln in chain if inner[0] <= ln <= inner[1]), None)
+                if sub is not None:
+                    key += f"/L{sub}"
+            out[key][classify(s.split()[0])] += 1
+    return out
+
+
 def main(asm_path: str, symbol: str) -> None:
     funcs = source_functions(SRC)
 
@@ -141,5 +180,24 @@ def main(asm_path: str, symbol: str) -> None:
         print(f"  {fi}:{ln:5d} {sum(c.values()):5d}  {dict(c.most_common(4))}  {src}")
 
 
+def print_stages(asm_path: str, symbol: str, root_line: int, outer: tuple, inner: tuple | None = None) -> None:
+    lines = SRC.read_text().splitlines()
+    st = stages(asm_path, symbol, root_line, outer, inner)
+    total = Counter()
+    print(f"stages of the code inlined at line {root_line} (stage = call line in {outer}, refined in {inner})")
+    print(f"{'stage':16s}" + "".join(f"{c:>9s}" for c in CLASSES) + f"{'total':>7s}  source")
+    for key in sorted(st, key=lambda k: [int(x[1:]) if x[1:].isdigit() else 0 for x in k.split("/")]):
+        c = st[key]
+        total.update(c)
+        ln = int(key.split("/")[-1][1:]) if key != "kernel" else 0
+        src = lines[ln - 1].strip()[:60] if ln else ""
+        print(f"{key:16s}" + "".join(f"{c[k]:9d}" for k in CLASSES) + f"{sum(c.values()):7d}  {src}")
+    print(f"{'TOTAL':16s}" + "".join(f"{total[k]:9d}" for k in CLASSES) + f"{sum(total.values()):7d}")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    if len(sys.argv) > 3:  # asm symbol root_line outer_a outer_b [inner_a inner_b]
+        a = [int(v) for v in sys.argv[3:]]
+        print_stages(sys.argv[1], sys.argv[2], a[0], (a[1], a[2]), (a[3], a[4]) if len(a) > 4 else None)
+    else:
+        main(sys.argv[1], sys.argv[2])
