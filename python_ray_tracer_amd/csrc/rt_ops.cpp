@@ -29,7 +29,7 @@
 //     RTX_FAST_MAX_BOUNCES), the workspace's status word is read back (a synchronisation) and
 //     cleared; RTX_ST_STACK_OVERFLOW raises RuntimeError("maximum recursion depth exceeded ...",
 //     where HipRenderer raises RecursionError), any other flag raises RuntimeError.
-// check=False keeps the op fully asynchronous (graph-capturable): the caller reads and clears the
+// check=False keeps the op fully asynchronous (no host synchronisation): the caller reads and clears the
 // flags later with rt::status(workspace).
 #include <ATen/ATen.h>
 #include <ATen/DeviceGuard.h>

@@ -32,8 +32,8 @@ Error channel of the render ops: with ``check=True`` (the default) a scene blob 
 disagrees with ``n_spheres`` raises before the launch (one small synchronous header copy), and a
 launch that may defer chains past the fast kernel's levels (max_bounces -1 or > 6) reads and clears
 the status word afterwards (a synchronisation), raising "maximum recursion depth exceeded" where
-HipRenderer raises RecursionError. ``check=False`` keeps the op asynchronous and
-graph-capturable; call ``rt::status(workspace)`` later. ``stats`` and ``workspace`` are declared
+HipRenderer raises RecursionError. ``check=False`` keeps the op asynchronous (no host
+synchronisation); call ``rt::status(workspace)`` later. ``stats`` and ``workspace`` are declared
 as mutated (``Tensor(a!)``, ``Tensor(b!)?``) and every op has a Meta (fake) kernel, so the ops
 trace under FakeTensor / torch.compile.
 
