@@ -234,11 +234,29 @@ class HipRenderer(Renderer):
         hit = self._scene_cache.get(key)
         if hit is None:
             blob = pack_key(*key)
-            hit = (torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True), int(blob[L.H_NSPH]))
-            if len(self._scene_cache) >= 16:
-                self._scene_cache.pop(next(iter(self._scene_cache)))
-            self._scene_cache[key] = hit
+            hit = self._cache_put(key, torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True),
+                                  int(blob[L.H_NSPH]))
+        return self._cache_ready(key, hit)
+
+    def _cache_put(self, key, dev_blob, n_spheres):
+        """Cache an uploaded blob with the event of its (asynchronous) upload: a launch on another
+        stream (TileGather's per-slot streams) waits for it until it is known complete."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        if len(self._scene_cache) >= 16:
+            self._scene_cache.pop(next(iter(self._scene_cache)))
+        hit = (dev_blob, n_spheres, ev)
+        self._scene_cache[key] = hit
         return hit
+
+    def _cache_ready(self, key, hit):
+        blob, n_spheres, ev = hit
+        if ev is not None:
+            if ev.query():  # uploaded: drop the event, later hits cost nothing
+                self._scene_cache[key] = (blob, n_spheres, None)
+            else:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+        return blob, n_spheres
 
     def workspace(self, n: int) -> torch.Tensor:
         need = int(self._lib.rtx_workspace_bytes(int(n), self._bounces_arg))
@@ -370,6 +388,16 @@ class HipRenderer(Renderer):
             self._scene_cache[ck] = hit
         return ck, hit
 
+    def fork(self) -> HipRenderer:
+        """A renderer sharing this one's settings, scene cache and stats buffer but with its own
+        workspace, so that its launches may run concurrently with this one's on another stream
+        (the workspace's counters and deferred lists belong to one launch at a time)."""
+        import copy
+
+        twin = copy.copy(self)
+        twin._ws = None
+        return twin
+
     @_on_device
     def _trace(self, ray_origin, dirs, scene) -> torch.Tensor:
         blob, S = self.scene_blob(scene)
@@ -440,11 +468,9 @@ class HipRenderer(Renderer):
         hit = self._scene_cache.get(key)
         if hit is None:
             blob = pack_override(scene, shape, shader)
-            hit = (torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True), int(blob[L.H_NSPH]))
-            if len(self._scene_cache) >= 16:
-                self._scene_cache.pop(next(iter(self._scene_cache)))
-            self._scene_cache[key] = hit
-        return hit
+            hit = self._cache_put(key, torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True),
+                                  int(blob[L.H_NSPH]))
+        return self._cache_ready(key, hit)
 
     @_on_device
     def _ray_directions(self, camera: Camera) -> torch.Tensor:

@@ -39,3 +39,43 @@ def test_two_ranks_share_gpu_gather_equals_single_frame(tmp_path):
     assert p.returncode == 0, (p.returncode, logs, p.stdout[-3000:], p.stderr[-3000:])
     assert set(logs) == {"rank0.txt", "rank1.txt"}, logs
     assert "False" not in logs["rank0.txt"] and "png_u8" in logs["rank0.txt"], logs
+
+
+def test_nccl_slots_on_streams_equal_single_frames():
+    """TileGather under nccl (a one-rank RCCL group on the box's one GPU): every slot renders on its
+    own stream with its own workspace and the root assembles on a side stream. Orbit frames pushed
+    through the two-slot pipeline (submit k, finish k-1), capped and unbounded, colour and uint8,
+    equal the single-GPU frames bit for bit; so does the synchronous one-slot path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.distributed import TileGather
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        base = scenes.random_spec(16, 5, 96, 61)
+        frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 12))) for k in range(6)]
+        for B, out in ((3, "u8"), (None, None)):
+            r = HipRenderer(max_bounces=B, color_dtype=torch.float32, device=dev)
+            want = [r.render_tile(sc, out=out).clone() for sc in frames]
+            tg = TileGather(r, 96, 61, row_block=4, out=out, slots=2)
+            assert tg.streams is not None
+            got, open_slot = [], None
+            for k, sc in enumerate(frames):
+                tg.submit(sc, k % 2)
+                if open_slot is not None:
+                    got.append(tg.finish(open_slot))
+                open_slot = k % 2
+            got.append(tg.finish(open_slot))
+            torch.cuda.synchronize()
+            for k in range(len(frames)):
+                assert torch.equal(got[k], want[k]), (B, k)
+            one = TileGather(r, 96, 61, row_block=4, out=out, slots=1)
+            assert one.streams is None and torch.equal(one.render(frames[2]), want[2])
+    finally:
+        dist.destroy_process_group()

@@ -52,6 +52,7 @@ def main():
     variants["eager"] = (eager, 1)
 
     s = torch.cuda.Stream(device=dev)
+    keep = []
     for F in [int(v) for v in a.frames_per_graph.split(",")]:
         bufs = [torch.empty_like(buf) for _ in range(F)]
         r.render_tile(scene, into=bufs[0])  # workspace sized, scene uploaded: nothing allocates in capture
@@ -64,6 +65,11 @@ def main():
         g.replay()
         torch.cuda.synchronize()
         ok = all(torch.equal(b, want) for b in bufs)
+        # the graph writes into bufs on every replay: keep them (and the graph) alive. (Rebinding
+        # bufs for the next F freed the previous graph's outputs, which the next capture's
+        # empty_cache() returned to the driver: its replays then wrote to unmapped memory — the
+        # illegal-address faults of sessions r3g and r3g2.)
+        keep.append((g, bufs))
         variants[f"graph x{F}"] = (g.replay, F)
         print(f"graph x{F}: captured, frames equal eager: {ok}", flush=True)
 
