@@ -1446,9 +1446,12 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   write_out(p, i, cr, cg, cb);
 }
 
-template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, bool TREE = true>
-__global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TREE ? kLvWaves : kLvWavesSmall)
+// TP: 0 = no culling tree and no persistent launch (scenes below kTreeMinSpheres), 1 = culling tree,
+// one tile per block (the launch is not persistent), 2 = both (persistent launches)
+template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2>
+__global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
                                                                    : kFastWavesPerSimd)) void k_render_fast(Params p0) {
+  constexpr bool TREE = TP >= 1;
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
@@ -1475,7 +1478,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
       return;
     }
   }
-  if (TREE && p.n_fetch > 0) {  // (persistent launches are for scenes of kPersistMinSpheres and more)
+  if (TP >= 2 && p.n_fetch > 0) {  // (persistent launches are for scenes of kPersistMinSpheres and more)
     // Persistent waves fetching kWaveW x kWaveH tiles, bottom-up (longest work first, as below).
     // Counter c (of n_fetch) hands out tiles c, c + n_fetch, ... . Waves are numbered XCD-major
     // (pw; block b runs on XCD b % 8) and wave pw uses counter pw % n_fetch, so every counter's
@@ -1961,14 +1964,20 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
 }
 
 // STATS: the instantiation with the per-level and executed-work counters (stats buffer given).
-// Scenes below kTreeMinSpheres carry no culling tree (scene_pack.BVH_MIN_SPHERES) and never take the
-// persistent launch: their instantiations (TREE = false) compile neither (A/B in DESIGN.md §4).
+// Launches that are not persistent run instantiations without the persistent tile loop (TP 1), and
+// scenes below kTreeMinSpheres, which carry no culling tree (scene_pack.BVH_MIN_SPHERES), ones
+// without the tree walks either (TP 0) (A/B in DESIGN.md §4).
 template <int B, bool DEEP, bool LVL, bool STATS>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
-  if (p.nsph < kTreeMinSpheres && p.n_fetch == 0) {
-    hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, false>), grid, dim3(kFastBlock), (uint32_t)lds,
-                          s, prof_event(0), prof_event(1), 0u, p);
+  if (p.n_fetch == 0) {  // one tile per block: the instantiations without the persistent loop
+    if (p.nsph < kTreeMinSpheres) {
+      hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0>), grid, dim3(kFastBlock), (uint32_t)lds, s,
+                            prof_event(0), prof_event(1), 0u, p);
+    } else {
+      hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 1>), grid, dim3(kFastBlock), (uint32_t)lds, s,
+                            prof_event(0), prof_event(1), 0u, p);
+    }
     return;
   }
   if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL, STATS>, lds, p);

@@ -51,6 +51,14 @@ def main():
         r.render_tile(scene, into=buf)
     variants["eager"] = (eager, 1)
 
+    def eager_new_out():
+        return r.render_tile(scene)
+    variants["eager new out"] = (eager_new_out, 1)
+
+    def bench_step():  # bench.py's step: the public API, a new output every frame
+        return r.raytrace_scene(scene.camera.position, r.get_ray_directions(scene.camera), scene)
+    variants["bench step"] = (bench_step, 1)
+
     s = torch.cuda.Stream(device=dev)
     keep = []
     for F in [int(v) for v in a.frames_per_graph.split(",")]:
