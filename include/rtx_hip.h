@@ -25,9 +25,9 @@
  *    x/y/z arrays of the reference's NumpyVector3D. A shared origin (the reference passes the
  *    camera position as Python scalars at level 0) is origin_stride == 0 and 3 doubles.
  *  - Work is enqueued asynchronously on `stream` (hipStream_t; NULL = the null stream); the caller
- *    synchronises. Entry points never allocate and never synchronise. They are NOT validated under
- *    HIP stream capture: a captured render_tile replayed correctly, but eager launches after the
- *    replays faulted (profiles/r3_ab_variants.txt, r3g); do not capture them into graphs.
+ *    synchronises. Entry points never allocate and never synchronise, so they can be captured into
+ *    a HIP graph (tools/graph_ab.py replays captured frames bit-identical to eager ones; the caller
+ *    keeps the graph's buffers alive); replays are no faster than eager launches here.
  *  - Return 0 on success, a negative RTX_E_* code otherwise; rtx_last_error() gives a message
  *    (thread-local). The Python layer raises RuntimeError on non-zero, like TORCH_CHECK would.
  *  - Scene blob: float64 array built by the host packer (scene_pack.py), layout below. It holds
