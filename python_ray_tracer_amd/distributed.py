@@ -11,11 +11,10 @@ all-gather would be bound by one link); the root un-permutes the rows with one d
 
 ``TileGather`` keeps its buffers across frames and lets frames overlap: ``submit(scene, slot)``
 enqueues the render and starts the gather asynchronously (the collective runs on the backend's own
-stream, after the render), ``finish(slot)`` assembles once the gather is done. Under nccl every
-slot renders on its own stream with its own workspace (``HipRenderer.fork``) and the root
-assembles on a side stream, so with two slots frame k+1 renders while frame k renders, gathers and
-is assembled: at 8 ranks a 1080p part is too small to fill the GPU alone. Under gloo
-(CPU tests, ranks sharing one GPU) tiles travel through host memory and every call is synchronous.
+stream, after the render), ``finish(slot)`` makes the current stream wait for it and assembles.
+With two slots the gather of frame k runs while frame k+1 renders (``bench.py --mode tiles``).
+Under gloo (CPU tests, ranks sharing one GPU) tiles travel through host memory and every call is
+synchronous.
 """
 
 from __future__ import annotations
@@ -54,65 +53,36 @@ class TileGather:
         coll = torch.device("cpu") if self.gloo else self.device
         self.recv = ([torch.zeros((self.world, plen), dtype=dtype, device=coll) for _ in range(slots)]
                      if self.rank == self.dst else None)
+        # the gather's per-rank views of each receive buffer, built once (not per frame)
+        self._recv_lists = [list(b.unbind(0)) for b in self.recv] if self.recv is not None else None
+        self._views = [b[:self.n].view(self.shape) for b in self.send]
         self._pending: dict = {}
-        # concurrent slots: nccl on a GPU with a renderer that can fork (its own workspace per slot)
-        self.streams = None
-        if not self.gloo and self.device.type == "cuda" and slots > 1 and hasattr(renderer, "fork"):
-            self.streams = [torch.cuda.Stream(device=self.device) for _ in range(slots)]
-            self.side = torch.cuda.Stream(device=self.device)
-            self.rs = [renderer] + [renderer.fork() for _ in range(slots - 1)]
 
     def submit(self, scene, slot: int = 0) -> None:
         """Render this rank's tile of ``scene`` into slot ``slot`` and start its gather."""
         if slot in self._pending:
             raise RuntimeError(f"slot {slot} still has a frame in flight: finish() it first")
-        if self.streams is not None:
-            # the slot's stream follows the caller's work and the slot's previous frame (its gather
-            # and assembly, both ordered before the side stream's current tail)
-            st = self.streams[slot]
-            st.wait_stream(torch.cuda.current_stream(self.device))
-            st.wait_stream(self.side)
-            with torch.cuda.stream(st):
-                self._submit(self.rs[slot], scene, slot)
-            return
-        self._submit(self.r, scene, slot)
-
-    def _submit(self, r, scene, slot):
         buf = self.send[slot]
-        view = buf[:self.n].view(self.shape)
+        view = self._views[slot]
         if self._into:
-            r.render_tile(scene, self.rb, self.world, self.rank, self.out, into=view)
+            self.r.render_tile(scene, self.rb, self.world, self.rank, self.out, into=view)
         else:  # a renderer without into= (test stand-ins): copy its tile in
-            view.copy_(r.render_tile(scene, self.rb, self.world, self.rank, self.out))
+            view.copy_(self.r.render_tile(scene, self.rb, self.world, self.rank, self.out))
         send = buf.cpu() if (self.gloo and buf.is_cuda) else buf
-        gl = list(self.recv[slot].unbind(0)) if self.rank == self.dst else None
+        gl = self._recv_lists[slot] if self.rank == self.dst else None
         work = self._dist.gather(send, gl, dst=self.dst, group=self.group, async_op=True)
         self._pending[slot] = (work, send)
 
     def finish(self, slot: int = 0):
         """Wait for slot ``slot``'s gather (a stream wait under nccl) and, on the root, assemble the
-        frame: [3, H*W] colour or [H, W, 3] uint8, ready on the caller's current stream. Other ranks
-        return None."""
+        frame: [3, H*W] colour or [H, W, 3] uint8. Other ranks return None."""
         work, _ = self._pending.pop(slot)
-        if self.streams is None:
-            work.wait()
-            if self.rank != self.dst:
-                return None
-            return self._assemble(self.r, slot)
-        cur = torch.cuda.current_stream(self.device)
-        with torch.cuda.stream(self.side):  # the gather's completion, then the un-permute, off the
-            work.wait()                     # caller's stream (it overlaps the next frame's render)
-            frame = self._assemble(self.r, slot) if self.rank == self.dst else None
-        if frame is None:
+        work.wait()
+        if self.rank != self.dst:
             return None
-        cur.wait_stream(self.side)
-        frame.record_stream(cur)
-        return frame
-
-    def _assemble(self, r, slot):
         tiles = self.recv[slot]
-        if hasattr(r, "assemble_rows"):  # HipRenderer: the device un-permute
-            return r.assemble_rows(tiles, self.W, self.H, self.rb, self.out)
+        if hasattr(self.r, "assemble_rows"):  # HipRenderer: the device un-permute
+            return self.r.assemble_rows(tiles, self.W, self.H, self.rb, self.out)
         return tiling.assemble(tiles, self.H, self.W, self.rb, self.out)
 
     def render(self, scene):

@@ -32,6 +32,7 @@ import torch
 
 from python_ray_tracer_amd.application import Renderer
 from python_ray_tracer_amd.domain import Camera, RGBColor, Vector3D
+from python_ray_tracer_amd.tiling import n_local_rows
 
 from . import _lib as L
 from .scene_pack import camera_words, pack_key, scene_key
@@ -195,8 +196,15 @@ def _on_device(method):
 
     @functools.wraps(method)
     def run(self, *args, **kwargs):
-        with torch.cuda.device(self.device):
+        idx = self.device.index
+        prev = torch.cuda.current_device()
+        if prev == idx:  # the common case: no device switch (and no context manager's cost)
             return method(self, *args, **kwargs)
+        torch.cuda.set_device(idx)
+        try:
+            return method(self, *args, **kwargs)
+        finally:
+            torch.cuda.set_device(prev)
     return run
 
 
@@ -234,29 +242,11 @@ class HipRenderer(Renderer):
         hit = self._scene_cache.get(key)
         if hit is None:
             blob = pack_key(*key)
-            hit = self._cache_put(key, torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True),
-                                  int(blob[L.H_NSPH]))
-        return self._cache_ready(key, hit)
-
-    def _cache_put(self, key, dev_blob, n_spheres):
-        """Cache an uploaded blob with the event of its (asynchronous) upload: a launch on another
-        stream (TileGather's per-slot streams) waits for it until it is known complete."""
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        if len(self._scene_cache) >= 16:
-            self._scene_cache.pop(next(iter(self._scene_cache)))
-        hit = (dev_blob, n_spheres, ev)
-        self._scene_cache[key] = hit
+            hit = (torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True), int(blob[L.H_NSPH]))
+            if len(self._scene_cache) >= 16:
+                self._scene_cache.pop(next(iter(self._scene_cache)))
+            self._scene_cache[key] = hit
         return hit
-
-    def _cache_ready(self, key, hit):
-        blob, n_spheres, ev = hit
-        if ev is not None:
-            if ev.query():  # uploaded: drop the event, later hits cost nothing
-                self._scene_cache[key] = (blob, n_spheres, None)
-            else:
-                torch.cuda.current_stream(self.device).wait_event(ev)
-        return blob, n_spheres
 
     def workspace(self, n: int) -> torch.Tensor:
         need = int(self._lib.rtx_workspace_bytes(int(n), self._bounces_arg))
@@ -314,8 +304,6 @@ class HipRenderer(Renderer):
         ``into``: a contiguous device tensor of that shape and dtype to render into (a
         pre-allocated gather buffer) instead of a new one. ``blob``/``n_spheres``: an already
         packed device scene (checked against its header)."""
-        from python_ray_tracer_amd.tiling import n_local_rows
-
         cam = scene.camera
         W, H = int(cam.width), int(cam.height)
         if blob is None:
@@ -388,16 +376,6 @@ class HipRenderer(Renderer):
             self._scene_cache[ck] = hit
         return ck, hit
 
-    def fork(self) -> HipRenderer:
-        """A renderer sharing this one's settings, scene cache and stats buffer but with its own
-        workspace, so that its launches may run concurrently with this one's on another stream
-        (the workspace's counters and deferred lists belong to one launch at a time)."""
-        import copy
-
-        twin = copy.copy(self)
-        twin._ws = None
-        return twin
-
     @_on_device
     def _trace(self, ray_origin, dirs, scene) -> torch.Tensor:
         blob, S = self.scene_blob(scene)
@@ -468,9 +446,11 @@ class HipRenderer(Renderer):
         hit = self._scene_cache.get(key)
         if hit is None:
             blob = pack_override(scene, shape, shader)
-            hit = self._cache_put(key, torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True),
-                                  int(blob[L.H_NSPH]))
-        return self._cache_ready(key, hit)
+            hit = (torch.from_numpy(blob).pin_memory().to(self.device, non_blocking=True), int(blob[L.H_NSPH]))
+            if len(self._scene_cache) >= 16:
+                self._scene_cache.pop(next(iter(self._scene_cache)))
+            self._scene_cache[key] = hit
+        return hit
 
     @_on_device
     def _ray_directions(self, camera: Camera) -> torch.Tensor:
@@ -518,7 +498,8 @@ class HipRenderer(Renderer):
         row_block, n_parts, p, out) flattened at its start. Returns what a whole-frame
         render_tile returns: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``)."""
         P = int(tiles.shape[0])
-        tiles = tiles.to(self.device).contiguous()
+        if tiles.device != self.device or not tiles.is_contiguous():
+            tiles = tiles.to(self.device).contiguous()
         if out == "u8":
             kind, res = L.OUT_U8_HWC, torch.empty((height, width, 3), dtype=torch.uint8, device=self.device)
         else:
