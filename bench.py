@@ -162,7 +162,10 @@ def main():
 
     # clock ramp (untimed): steps until --ramp-ms has passed, synchronising every 32 so the host does
     # not queue far ahead; then the W warm-up steps and the timed region as the contract says
-    n_ramp = 0
+    step()  # the first call loads the code object and uploads the scene: not part of the ramp's time
+    drain()
+    torch.cuda.synchronize(dev)
+    n_ramp = 1
     t_ramp = time.perf_counter()
     while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
         step()

@@ -24,7 +24,8 @@ def per_launch(d: Path, counter: str) -> float | None:
             for row in csv.DictReader(fh):
                 name = row["Kernel_Name"]
                 tmpl = name.split("k_render_fast<", 1)[-1].split(">", 1)[0] if "k_render_fast<" in name else ""
-                if tmpl.endswith("false") and row["Counter_Name"] == counter:
+                args = [t.strip() for t in tmpl.split(",")]
+                if len(args) >= 5 and args[4] == "false" and row["Counter_Name"] == counter:  # STATS = false
                     vals.append(float(row["Counter_Value"]))
     return statistics.median(vals) if vals else None
 
@@ -33,16 +34,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--keep", default="", help="configs whose previous entries stay (kernel unchanged since)")
     a = ap.parse_args()
     root = Path(a.root)
     out = Path(a.out)
     old = json.loads(out.read_text()) if out.exists() else {}
-    res = {k: v for k, v in old.items() if k.startswith("_")}
+    keep = set(a.keep.split(",")) if a.keep else set()
+    res = {k: v for k, v in old.items() if k.startswith("_") or k in keep}
     res["_source"] = (f"median per k_render_fast launch (timed instantiation, STATS=false), rocprofv3 --pmc "
                       f"FETCH_SIZE / WRITE_SIZE in separate runs of bench.py, {root}")
     for c, px in FRAME_PX.items():
-        rd = per_launch(root / f"{c}_fetch", "FETCH_SIZE")
-        wr = per_launch(root / f"{c}_write", "WRITE_SIZE")
+        rd = per_launch(root / f"{c}_fetch", "FETCH_SIZE") or per_launch(root / f"pmc_{c}" / "fetch", "FETCH_SIZE")
+        wr = per_launch(root / f"{c}_write", "WRITE_SIZE") or per_launch(root / f"pmc_{c}" / "write", "WRITE_SIZE")
         if rd is None or wr is None:
             continue
         frame = 12 * px
@@ -50,8 +53,6 @@ def main():
                   "fetch_bytes_x2": round(rd * 2048), "write_bytes": round(wr * 1024),
                   "hbm_bytes_per_launch": round(rd * 2048 + wr * 1024), "frame_bytes": frame,
                   "traffic_over_frame": round((rd * 2048 + wr * 1024) / frame, 3)}
-        if c == "C2" and "variant_4_waves_per_simd_no_spills" in old.get("C2", {}):
-            res[c]["variant_4_waves_per_simd_no_spills"] = old["C2"]["variant_4_waves_per_simd_no_spills"]
     out.write_text(json.dumps(res, indent=1))
     for c in FRAME_PX:
         if c in res:

@@ -2,7 +2,11 @@
 warm-up, timed region and the bench's extra launches (the counter launch and the output-path
 renders), to compare with the bench line's live ``roofline.kernel_ms``.
 
-    python tools/rocprof_summary.py gpurun_out/<tag>/prof --warmup 10 --steps 100
+    python tools/rocprof_summary.py gpurun_out/<tag>/prof --warmup 10 --steps 100 [--ramp 1700]
+    python tools/rocprof_summary.py gpurun_out/<tag>/prof --log gpurun_out/<tag>/rocprof.log
+
+``--log``: the profiled bench.py's output, whose JSON line gives the clock-ramp launches (bench.py
+--ramp-ms runs untimed steps before the warm-up), the warm-up and the timed steps.
 """
 
 import argparse
@@ -18,10 +22,24 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--kernel", default="k_render_fast")
     ap.add_argument("--prof-every", type=int, default=10, help="bench.py's sampling stride")
+    ap.add_argument("--ramp", type=int, default=0, help="launches of bench.py's clock ramp (before the warm-up)")
+    ap.add_argument("--log", default=None, help="bench.py's output: ramp, warm-up and steps from its JSON line")
     a = ap.parse_args()
+    if a.log:
+        import json
+
+        for line in open(a.log, errors="replace"):
+            if line.startswith("{") and '"metric"' in line:
+                d = json.loads(line)
+                a.warmup, a.steps = d["warmup"], d["steps"]
+                a.ramp = d.get("ramp", {}).get("steps", 0)
     rows = [r for r in csv.DictReader(open(Path(a.prof_dir) / "run_kernel_trace.csv")) if a.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+    if a.ramp:  # the clock ramp's launches precede the warm-up
+        print(f"clock ramp: {a.ramp} launches, mean {statistics.mean(d[:a.ramp]):.2f} us, last 10 mean "
+              f"{statistics.mean(d[max(0, a.ramp - 10):a.ramp]):.2f} us")
+        rows, d = rows[a.ramp:], d[a.ramp:]
     timed = d[a.warmup:a.warmup + a.steps]
     print(f"kernel {rows[0]['Kernel_Name']}")
     print(f"launches: {len(d)} (warm-up {a.warmup}, timed {len(timed)}, after {len(d) - a.warmup - len(timed)})")
