@@ -546,3 +546,26 @@ def test_textured_row_tiles_reassemble(hip, B):
             shp = tiling.tile_shape(61, 96, rb, P, p, None)
             r.render_tile(scene, rb, P, p, into=buf[p, :int(np.prod(shp))].view(shp))
         assert torch.equal(r.assemble_rows(buf, 96, 61, rb, None), full), (B, P, rb)
+
+
+@pytest.mark.parametrize("B", [3, 4, None])
+def test_small_scene_with_a_tree_renders_without_it(hip, B):
+    """Scenes below 8 spheres run the TP = 0 kernel, which compiles no culling-tree walk. A blob of
+    such a scene that carries a tree anyway (packed with BVH_MIN_SPHERES lowered) must render what
+    the linear loops render — the tree only culls — and equal the oracle."""
+    from python_ray_tracer_amd.infrastructure.hip import scene_pack as P
+
+    spec = scenes.random_spec(5, 7, 64, 40)  # 6 spheres with the ground
+    old = P.BVH_MIN_SPHERES
+    try:
+        P.BVH_MIN_SPHERES = 2
+        P._pack_static.cache_clear()
+        r, got = _render(hip, spec, B)
+        assert r.scene_blob(scenes.build_scene(spec))[0][P.L.H_NNODES].item() > 0  # the tree is there
+    finally:
+        P.BVH_MIN_SPHERES = old
+        P._pack_static.cache_clear()
+    want = O.render(O.scene_from_spec(spec), B)
+    assert np.abs(got - want).max() <= ATOL
+    _, plain = _render(hip, spec, B)
+    assert np.array_equal(got, plain)
