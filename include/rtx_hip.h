@@ -223,6 +223,23 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
                       int max_bounces, void* out, int out_kind,
                       void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream);
 
+/* rtx_render_camera with options for callers that render the same frame repeatedly:
+ *  - deferred_out (may be NULL): a device-accessible uint32 (device memory, or mapped host memory)
+ *    that receives, in stream order, the number of rays the fast kernel deferred in this launch
+ *    (ties, longer chains); written by the general kernel, so it is left untouched when that kernel
+ *    is skipped;
+ *  - flags RTX_F_NO_GENERAL: for a capped render (0 <= max_bounces <= RTX_FAST_MAX_BOUNCES) whose
+ *    identical earlier launch (same blob content, tile, cap) deferred no ray, the general kernel is
+ *    not launched (the render is deterministic, so it defers none again). Passing it for a render
+ *    that does defer rays leaves those pixels unwritten and the workspace counters non-zero: the
+ *    caller guarantees it. Uncapped renders ignore it. */
+#define RTX_F_NO_GENERAL 1u
+int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int height,
+                         int row_block, int n_parts, int part, int n_local_rows,
+                         int max_bounces, void* out, int out_kind,
+                         void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream,
+                         unsigned flags, uint32_t* deferred_out);
+
 /* Animation / batch driver (the reference renders one frame per
  * render_image_pipeline call, application.py:43-52): n_frames whole frames of one size, sphere
  * count and bounce cap in ONE launch. Frame f reads the blob at scenes + f * scene_stride (words;

@@ -167,6 +167,7 @@ struct Params {
   int64_t scene_stride;
   int n_frames;
   int frame;  // set per block / per deferred ray (kernel side)
+  uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null
 };
 
 // Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
@@ -1684,6 +1685,7 @@ __global__ __launch_bounds__(64) void k_render_general(Params p0) {
   // Nothing deferred in this launch (the rule for capped renders): every counter is already zero,
   // so there is nothing to render and nothing to reset, and no block touches the done counter
   // (its 64 returning atomics on one address were most of this launch's 5 us).
+  if (p.deferred_out && blockIdx.x == 0 && threadIdx.x == 0) *p.deferred_out = hdr[RTX_WS_COUNT];  // before any reset
   if (hdr[RTX_WS_COUNT] == 0u && hdr[RTX_WS_COUNT2] == 0u && hdr[RTX_WS_COUNT3] == 0u) return;
   int64_t count = (int64_t)*p.in_count;
   if (count > p.list_cap) count = p.list_cap;
@@ -2043,7 +2045,8 @@ void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
 }
 static_assert(RTX_FAST_MAX_BOUNCES == 6, "launch_fast switch covers 0..6");
 
-int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s) {
+// no_general: the caller knows this exact (capped) render defers no ray (rtx_render_camera_ex)
+int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {
   if (p.nsph <= 0 || p.nsph > RTX_MAX_SPHERES) return fail(RTX_E_ARG, "n_spheres out of range%s (%lld)", "", p.nsph);
   if (!p.scene || !p.out || !workspace) return fail(RTX_E_ARG, "null pointer argument%s", "");
   if (p.out_kind < 0 || p.out_kind > 2) return fail(RTX_E_ARG, "bad out_kind%s %lld", "", p.out_kind);
@@ -2136,6 +2139,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     }
   }
   // deferred rays: ties, and chains longer than the fast kernel's levels
+  if (no_general && capped) return RTX_OK;
   hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);
   return check_launch("k_render_general");
 }
@@ -2199,12 +2203,14 @@ size_t rtx_workspace_bytes(int64_t n_rays, int max_bounces) {
   return ws_bytes(n_rays, max_bounces);
 }
 
-int rtx_render_camera(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
-                      int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
-                      size_t workspace_bytes, uint64_t* stats, void* stream) {
+int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
+                         int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
+                         size_t workspace_bytes, uint64_t* stats, void* stream, unsigned flags,
+                         uint32_t* deferred_out) {
   if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
       n_local_rows < 0 || n_local_rows > height)
     return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  if (flags & ~(unsigned)RTX_F_NO_GENERAL) return fail(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
   Params p{};
   p.scene = scene;
   p.nsph = n_spheres;
@@ -2220,7 +2226,15 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
   p.out = out;
   p.out_kind = out_kind;
   p.stats = (unsigned long long*)stats;
-  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream);
+  p.deferred_out = deferred_out;
+  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream, (flags & RTX_F_NO_GENERAL) != 0);
+}
+
+int rtx_render_camera(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
+                      int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
+                      size_t workspace_bytes, uint64_t* stats, void* stream) {
+  return rtx_render_camera_ex(scene, n_spheres, width, height, row_block, n_parts, part, n_local_rows, max_bounces,
+                              out, out_kind, workspace, workspace_bytes, stats, stream, 0u, nullptr);
 }
 
 int rtx_render_frames(const double* scenes, int64_t scene_stride, int n_frames, int n_spheres, int width, int height,

@@ -41,6 +41,8 @@ ST_STACK_OVERFLOW = 1
 ST_LIST_OVERFLOW = 2
 ST_BAD_SCENE = 4
 
+F_NO_GENERAL = 1  # rtx_render_camera_ex flags
+
 # header words
 H_MAGIC, H_NSPH, H_CAM, H_LIGHT, H_DOMEC, H_NDOME, H_DOMEI = 0, 1, 2, 5, 8, 11, 12
 H_XSTART, H_XSTEP, H_XSTOP, H_XFIX = 20, 21, 22, 23
@@ -65,6 +67,7 @@ EXPORTS = (
     "rtx_last_error",
     "rtx_workspace_bytes",
     "rtx_render_camera",
+    "rtx_render_camera_ex",
     "rtx_render_frames",
     "rtx_trace_rays",
     "rtx_ray_directions",
@@ -89,6 +92,8 @@ _SIGS = {
     "rtx_workspace_bytes": (_size, [_i64, _i32]),
     "rtx_render_camera": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
                                  _c_void_p, _size, _c_void_p, _c_void_p]),
+    "rtx_render_camera_ex": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
+                                    _c_void_p, _size, _c_void_p, _c_void_p, ctypes.c_uint, _c_void_p]),
     "rtx_render_frames": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p, _size,
                                  _c_void_p, _c_void_p]),
     "rtx_trace_rays": (_i32, [_c_void_p, _i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i32, _c_void_p,

@@ -94,6 +94,47 @@ def test_ties_take_the_general_kernel(hip, golden_meta, golden_renders):
     assert r.stats()["rays"] == st.rays and r.stats()["hits"] == st.hits
 
 
+@pytest.mark.parametrize("case", ["ties_64x36_B2", "main_160x90_B3", "rand16_128x72_B4"])
+def test_general_launch_skipped_only_when_nothing_is_deferred(hip, golden_meta, golden_renders, case):
+    """HipRenderer probes the deferred count of a capped render's first launch and skips the
+    general kernel (RTX_F_NO_GENERAL) on later renders of the same scene only if it was 0; every
+    render still equals the golden one (the tie scene keeps its general launch)."""
+    c = golden_meta["cases"][case]
+    r = hip.HipRenderer(max_bounces=c["max_bounces"])
+    scene = scenes.build_scene(c["spec"])
+    for _ in range(3):
+        got = r.render_tile(scene).cpu().numpy()  # .cpu() synchronises: the probe has landed
+        assert np.abs(got - golden_renders[case]).max() <= ATOL
+    (state,) = r._defers.values()
+    assert state is (case != "ties_64x36_B2")
+    # the skip is per tile: another part of the same scene probes on its own
+    r.render_tile(scene, 8, 2, 1)
+    assert len(r._defers) == 2
+    # another camera is another key
+    spec2 = {**c["spec"], "camera": {**c["spec"]["camera"], "position": [0.05, 0.3, -2.0]}}
+    r.render_tile(scenes.build_scene(spec2))
+    assert len(r._defers) == 3
+
+
+def test_camera_ex_flags_are_checked(hip):
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    r = hip.HipRenderer(max_bounces=2)
+    scene = scenes.build_scene(scenes.random_spec(4, 0, 16, 8))
+    blob, S = r.scene_blob(scene)
+    out = torch.empty((3, 128), dtype=torch.float64, device="cuda")
+    ws = r.workspace(128)
+    rc = r._lib.rtx_render_camera_ex(blob.data_ptr(), S, 16, 8, 1, 1, 0, 8, 2, out.data_ptr(), L.OUT_F64_SOA,
+                                     ws.data_ptr(), ws.numel(), None, L.stream_handle(), 2, None)
+    assert rc != 0 and b"flags" in r._lib.rtx_last_error()
+    # the deferred count lands in a device word: 0 for a tie-free scene
+    cnt = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    L.check(r._lib.rtx_render_camera_ex(blob.data_ptr(), S, 16, 8, 1, 1, 0, 8, 2, out.data_ptr(), L.OUT_F64_SOA,
+                                        ws.data_ptr(), ws.numel(), None, L.stream_handle(), 0, cnt.data_ptr()),
+            "rtx_render_camera_ex")
+    assert int(cnt.item()) == 0
+
+
 @pytest.mark.parametrize("B", [0, 1, 2, 4, 5, 6, 7, 8, 9, 12])
 def test_every_bounce_cap(hip, B):
     spec = scenes.random_spec(16, 0, 128, 72)

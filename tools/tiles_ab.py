@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--profile", action="store_true", help="cProfile the steps of the last height")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -83,6 +84,19 @@ def main():
                 torch.cuda.synchronize()
                 times[name].append((time.perf_counter() - t0) / a.steps * 1e6)
                 assert torch.equal(state["last"], want), (H, name)
+        if a.profile and H == int(a.heights.split(",")[-1]):
+            import cProfile
+            import pstats
+
+            step, drain, _ = variants["pipeline"]
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(a.steps):
+                step()
+            drain()
+            pr.disable()
+            torch.cuda.synchronize()
+            pstats.Stats(pr).sort_stats("tottime").print_stats(25)
         for name, ts in times.items():
             ts.sort()
             res[f"{W}x{H} {name}"] = {"best_us_per_step": round(ts[0], 2), "median_us_per_step": round(ts[len(ts) // 2], 2)}
