@@ -88,12 +88,18 @@ enum {
   RTX_H_TAME = 37,   /* 1: every coordinate (centres, camera) and radius below 2^60 in magnitude, so
                         the fast kernel may use the half-b sphere test (rtx_kernels.hip SphTest); 0: the
                         reference expressions everywhere */
-  RTX_H_MAT0 = 38    /* rtx_shade_hits only: word offset of a material record (RTX_MAT_WORDS) that
+  RTX_H_MAT0 = 38,   /* rtx_shade_hits only: word offset of a material record (RTX_MAT_WORDS) that
                         replaces the shape's own at level 0 — NumpyShader.create called on another
                         shape's shader (shader.py:63-112 reads self.* for the hit, and traces the
                         reflections through the unchanged scene, :152); 0 = none */
+  RTX_H_SHGRID = 39  /* optional shadow grid (scenes with a culling tree and at most 128 spheres): word
+                        offset of its record, 0 = none. Record: lo x,y,z; 1/cell x,y,z; nx, ny, nz;
+                        then per voxel (x fastest) two 64-bit masks stored as the bits of two doubles:
+                        bit j of mask k set unless sphere 64k+j provably cannot shadow (shader.py:126-128
+                        in its any-hit form) a shadow ray whose nudged origin lies in the voxel */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
+#define RTX_SHGRID_WORDS 9  /* words of the shadow-grid record before its masks */
 
 /* per-sphere geometry words */
 enum {

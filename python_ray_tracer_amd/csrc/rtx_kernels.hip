@@ -959,6 +959,69 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   cb = (ab + xb) + ib;
 }
 
+// ---- shadow grid (RTX_H_SHGRID, scene_pack._append_shadow_grid) ---------------------------
+// The union, over the wave's lanes, of the voxel masks of their nudged hit points q: the spheres
+// that may shadow any of them. False (use the culling tree) when some lane's q lies outside the
+// grid, has |N|^2 > 4 (the grid's nudge bound) or is NaN, or when the lanes span more than
+// kGridWaterfall voxels.
+constexpr int kGridWaterfall = 8;
+__device__ __forceinline__ bool grid_mask(const cdouble* sc, double qx, double qy, double qz, double n2, uint64_t& m0,
+                                          uint64_t& m1) {
+  const cdouble* gr = sc + (int)sc[RTX_H_SHGRID];
+  const double fx = (qx - gr[0]) * gr[3], fy = (qy - gr[1]) * gr[4], fz = (qz - gr[2]) * gr[5];
+  const bool in = fx >= 0.0 && fx < gr[6] && fy >= 0.0 && fy < gr[7] && fz >= 0.0 && fz < gr[8] && n2 <= 4.0;
+  if (__ballot(!in) != 0) return false;
+  const int key = ((int)fz * (int)gr[7] + (int)fy) * (int)gr[6] + (int)fx;
+  const cdouble* masks = gr + RTX_SHGRID_WORDS;
+  m0 = 0;
+  m1 = 0;
+  bool pend = true;
+  for (int it = 0;; ++it) {
+    const uint64_t b = __ballot(pend);
+    if (b == 0) return true;
+    if (it == kGridWaterfall) return false;
+    const int k0 = __builtin_amdgcn_readlane(key, (int)__builtin_ctzll(b));
+    m0 |= (uint64_t)__double_as_longlong(masks[2 * k0]);
+    m1 |= (uint64_t)__double_as_longlong(masks[2 * k0 + 1]);
+    pend = pend && key != k0;
+  }
+}
+
+// Shadow any-hit over the candidate spheres of masks m0/m1 (scene order, pairs), skipping the
+// wave-uniform own shape hs: lit stays true unless some candidate is strictly nearer than t_self.
+template <typename G, typename Wk>
+__device__ __forceinline__ bool lit_masked(const G* geo, uint64_t m0, uint64_t m1, int hs, double qx, double qy,
+                                           double qz, double qq, double lx, double ly, double lz, double tself,
+                                           double tame, Wk& wk) {
+  if (hs < 64) m0 &= ~(uint64_t(1) << hs);
+  else if (hs < 128) m1 &= ~(uint64_t(1) << (hs - 64));
+  wk.test(__builtin_popcountll(m0) + __builtin_popcountll(m1));
+  bool lit = true;
+  for (int half = 0; half < 2; ++half) {
+    uint64_t m = half ? m1 : m0;
+    const int base = half * 64;
+    while (m) {
+      const int s0 = base + __builtin_ctzll(m);
+      m &= m - 1;
+      const SphTest a0 = isect_disc(geo + s0 * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz, tame);
+      if (m) {
+        const int s1 = base + __builtin_ctzll(m);
+        m &= m - 1;
+        isect_pair(a0, isect_disc(geo + s1 * RTX_GEOM_WORDS, qx, qy, qz, qq, lx, ly, lz, tame),
+                   [&](double t0, bool v0, double t1, bool v1) {
+                     if ((v0 && t0 < tself) || (v1 && t1 < tself)) lit = false;
+                   });
+      } else {
+        isect_one(a0, [&](double t0, bool v0) {
+          if (v0 && t0 < tself) lit = false;
+        });
+      }
+      if (__ballot(lit) == 0) return false;  // every lane of the wave is in shadow
+    }
+  }
+  return lit;
+}
+
 // NumpyShader.create (shader.py:63-112) for a hit of sphere h at distance t, minus the colour
 // assembly (hit_color) and the reflection recursion (driven by the caller).
 // geo: scalar-cache view of the sphere table (wave-uniform loops); tab: the per-lane view of the
@@ -995,7 +1058,15 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   const int h0 = __builtin_amdgcn_readfirstlane(h);
   const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
   const bool culled = TREE && sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
-  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
+  if (culled) {
+    uint64_t m0, m1;
+    if (sc[RTX_H_SHGRID] != 0.0 && grid_mask(sc, qx, qy, qz, dot3(nx, ny, nz, nx, ny, nz), m0, m1)) {
+      wk.node();  // the voxel lookup, priced as one node test
+      lit = lit_masked(geo, m0, m1, hs, qx, qy, qz, qq, lx, ly, lz, tself, tame, wk);
+    } else {
+      lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
+    }
+  }
   const int nshadow = culled ? 0 : nsph - (hs < nsph);
   int j = 0;
   for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
@@ -1106,6 +1177,104 @@ __device__ __forceinline__ void camera_ray(const Params& p, int col, int lr, dou
   ox = sc[RTX_H_CAM + 0];
   oy = sc[RTX_H_CAM + 1];
   oz = sc[RTX_H_CAM + 2];
+}
+
+// ---- level-0 candidates of a wave tile ------------------------------------------------------
+// The camera rays of a wave's pixels leave one origin O through points (x, y, 0) of the image
+// plane (camera_dir, base.py:123-141), and x (y) is monotone in the column (row), as is its
+// rounding, so every lane's vector v = (fl(x - Ox), fl(y - Oy), VZ) lies in the rectangle spanned
+// by the four corner vectors of the tile's extreme columns and rows. The rays therefore lie in the
+// pyramid bounded by the four planes through O and two adjacent corners. A sphere whose ball,
+// expanded by the culling margin lm (node_may_hit: a root the reference reports lies within lm of
+// the ball), is wholly outside one of those planes yields FARAWAY for every ray of the tile, so
+// the tile's level-0 nearest hit may skip it: with scale = |C - O|^2 + 2|C|^2 + 3r^2 + |O|^2
+// (>= node_may_hit's scale for a single sphere), lm = 1e-7 (scale + 1), doubled here like the
+// node margin (it also absorbs the rounding of the corner cross products and dot products,
+// ~1e-15 relative, and |D| = 1 +- 1e-15). Comparisons are written so that NaN keeps the sphere.
+// One lane tests one sphere (two passes for 65..128 spheres); the ballots are the tile's candidate
+// masks. Needs the full wave (call before any lane diverges).
+__device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, uint64_t& m0, uint64_t& m1) {
+  const cdouble* sc = (const cdouble*)p.scene;
+  const int W = p.width;
+  if (c0 >= W || lr0 >= p.n_rows) return false;  // no pixel of this wave lies in the frame
+  const int c1 = c0 + kWaveW - 1 < W - 1 ? c0 + kWaveW - 1 : W - 1;
+  const int l1 = lr0 + kWaveH - 1 < p.n_rows - 1 ? lr0 + kWaveH - 1 : p.n_rows - 1;
+  const int H = p.height;
+  auto xv = [&](int c) {
+    return (sc[RTX_H_XFIX] != 0.0 && c == W - 1) ? sc[RTX_H_XSTOP] : (double)c * sc[RTX_H_XSTEP] + sc[RTX_H_XSTART];
+  };
+  auto yv = [&](int r) {
+    return (sc[RTX_H_YFIX] != 0.0 && r == H - 1) ? sc[RTX_H_YSTOP] : (double)r * sc[RTX_H_YSTEP] + sc[RTX_H_YSTART];
+  };
+  const double xa = xv(c0), xb = xv(c1), ya = yv(global_row(p, lr0)), yb = yv(global_row(p, l1));
+  const double ox = sc[RTX_H_CAM + 0], oy = sc[RTX_H_CAM + 1], oz = sc[RTX_H_CAM + 2];
+  const double x0 = __builtin_fmin(xa, xb) - ox, x1 = __builtin_fmax(xa, xb) - ox;
+  const double y0 = __builtin_fmin(ya, yb) - oy, y1 = __builtin_fmax(ya, yb) - oy;
+  const double v = sc[RTX_H_VZ];
+  // corners A (x0, y0), B (x1, y0), C (x1, y1), D (x0, y1), counter-clockwise in the image plane;
+  // n = sign(VZ) (a x b) points into the pyramid for each edge (a, b)
+  const double sg = v > 0.0 ? 1.0 : -1.0;
+  const double ax[4] = {x0, x1, x1, x0}, ay[4] = {y0, y0, y1, y1};
+  double nx[4], ny[4], nz[4], nl[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = (k + 1) & 3;
+    nx[k] = sg * ((ay[k] * v) - (v * ay[j]));
+    ny[k] = sg * ((v * ax[j]) - (ax[k] * v));
+    nz[k] = sg * ((ax[k] * ay[j]) - (ay[k] * ax[j]));
+    nl[k] = __builtin_sqrt((nx[k] * nx[k] + ny[k] * ny[k]) + nz[k] * nz[k]);
+  }
+  const double oo = sc[RTX_H_CAMOO];
+  const double* g = p.scene + RTX_HDR_WORDS;  // per-lane loads: a generic pointer
+  const int lane = (int)__lane_id();
+  auto may = [&](int s) {
+    if (s >= p.nsph) return false;
+    const double* e = g + s * RTX_GEOM_WORDS;
+    const double wx = e[RTX_G_CX] - ox, wy = e[RTX_G_CY] - oy, wz = e[RTX_G_CZ] - oz;
+    const double rr = e[RTX_G_RR];
+    const double scale = (((wx * wx + wy * wy) + wz * wz) + 2.0 * e[RTX_G_CC]) + 3.0 * rr + oo;
+    const double m = __builtin_sqrt(rr) + 2e-7 * (scale + 1.0);
+    bool out = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out = out || ((nx[k] * wx + ny[k] * wy) + nz[k] * wz < -(m * nl[k]));
+    return !out;
+  };
+  m0 = __ballot(may(lane));
+  m1 = p.nsph > 64 ? __ballot(may(64 + lane)) : 0ull;
+  return true;
+}
+
+// Nearest hit of camera rays over the candidate spheres of masks m0 (spheres 0..63) and m1
+// (64..127), in scene order, pairs at a time like nearest_hit.
+template <typename P, typename Wk>
+__device__ __forceinline__ void nearest_masked(const P* geo, uint64_t m0, uint64_t m1, double ox, double oy,
+                                               double oz, double dx, double dy, double dz, double& tmin, int& hit,
+                                               bool& tie, double tame, Wk& wk) {
+  wk.test(__builtin_popcountll(m0) + __builtin_popcountll(m1));
+  tmin = FARAWAY;
+  hit = -1;
+  tie = false;
+  auto run = [&](uint64_t m, int base) {
+    while (m) {
+      const int s0 = base + __builtin_ctzll(m);
+      m &= m - 1;
+      const P* g0 = geo + s0 * RTX_GEOM_WORDS;
+      const SphTest a0 = isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame);
+      if (m) {
+        const int s1 = base + __builtin_ctzll(m);
+        m &= m - 1;
+        const SphTest a1 = isect_disc_cam(geo + s1 * RTX_GEOM_WORDS, ox, oy, oz, dx, dy, dz, tame);
+        isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
+          nearest_update(v0, t0, s0, tmin, hit, tie);
+          nearest_update(v1, t1, s1, tmin, hit, tie);
+        });
+      } else {
+        isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s0, tmin, hit, tie); });
+      }
+    }
+  };
+  run(m0, 0);
+  run(m1, 64);
 }
 
 __device__ __forceinline__ void load_ray(const Params& p, int64_t i, double& ox, double& oy, double& oz, double& dx,
@@ -1222,6 +1391,17 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   double tmin = FARAWAY;
   int hit = -1;
   bool tie = false;
+  // level-0 candidate spheres of the wave tile (wave_frustum) instead of the culling tree: camera
+  // rays of a tame scene with a tree and at most 128 spheres
+  uint64_t fm0 = 0, fm1 = 0;
+  bool fr = false;
+  if constexpr (TREE) {
+    if (cam0 && nsph <= 128 && sc[RTX_H_NNODES] != 0.0 && sc[RTX_H_TAME] != 0.0 && sc[RTX_H_VZ] != 0.0) {
+      const int lane = threadIdx.x & 63;
+      fr = wave_frustum(p, __builtin_amdgcn_readfirstlane(col - lane % kWaveW),
+                        __builtin_amdgcn_readfirstlane(lr - lane / kWaveW), fm0, fm1);
+    }
+  }
   if (active) {
     if (rin) {
       ox = rin[0]; oy = rin[1]; oz = rin[2];
@@ -1245,7 +1425,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       // with that material, deferred like a tie
       tie = sc[RTX_H_MAT0] != 0.0;
     } else if (TREE && sc[RTX_H_NNODES] != 0.0) {
-      if (cam0) {
+      if (fr) {
+        wk.node();  // the tile's plane tests, priced as two node tests per 64 spheres
+        wk.node();
+        if (nsph > 64) {
+          wk.node();
+          wk.node();
+        }
+        nearest_masked(geo, fm0, fm1, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+      } else if (cam0) {
         nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else {
         nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);

@@ -162,6 +162,8 @@ def _pack_static(static: tuple) -> np.ndarray:
     blob[L.HDR_WORDS + S * L.GEOM_WORDS:] = np.asarray(mat_rows, dtype=np.float64).ravel()
     if S >= BVH_MIN_SPHERES:
         blob = _append_culling_tree(blob, geo.copy(), S)
+        if S <= SHGRID_MAX_SPHERES:
+            blob = _append_shadow_grid(blob, geo.copy(), S, lpos)
     # image textures: one float64 RGB texel table per distinct image, after everything else; the
     # material's RTX_M_TR word holds its word offset
     textures, offsets, size = [], {}, blob.size
@@ -367,6 +369,79 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
     out[L.H_NALWAYS] = len(huge)
     out[L.H_NODES] = hdr_nodes
     out[L.H_CGEO] = hdr_cgeo
+    return out
+
+
+# --- shadow grid -----------------------------------------------------------------------------
+# _calculate_shadow (shader.py:114-128) casts, from the nudged hit point q = p + 1e-4 N, a ray along
+# L_dir = norm(light - p) and tests every sphere. Its line passes through q and, since its direction
+# is that of light - p, through light + (q - p), within 1e-4 |N| of the light. For a voxel V of a grid
+# over the small spheres, every such line with q in V therefore lies within eps_n of the double cone
+# with apex at the light around V's bounding ball grown by eps_n (the kernel only uses the grid when
+# every lane has |N|^2 <= 4, so eps_n = 2e-4). A sphere farther from that cone than its radius plus
+# the reference formula's rounding reach (a root it reports lies within lm <= 1.8e-7 (|C| + |q| + r)
+# of the ball, the same budget as node_may_hit; 1e-6 (... + 1) here) yields FARAWAY on every such
+# ray and cannot shadow: the voxel's mask leaves it out. Distance of a point at w from the light to
+# the double cone of unit axis a and half-angle T: |w x a| cos T - |w.a| sin T (for w outside it).
+SHGRID_MAX_SPHERES = 128
+SHGRID_CELLS = 24  # cells along the grid's longest side (cubic cells)
+SHGRID_MAX_VOXELS = 1 << 14
+
+
+def _append_shadow_grid(blob: np.ndarray, geo: np.ndarray, S: int, lpos) -> np.ndarray:
+    light = np.asarray(lpos, dtype=np.float64)
+    centers = geo[:, L.G_CX:L.G_CZ + 1]
+    radii = np.sqrt(geo[:, L.G_RR])
+    if not (np.all(np.isfinite(light)) and np.all(np.isfinite(centers)) and np.all(np.isfinite(radii))):
+        return blob
+    small = [i for i in range(S) if not (radii[i] > HUGE_RADIUS or float(np.abs(centers[i]).max()) > 1e4)]
+    if not small:
+        return blob
+    lo = (centers[small] - radii[small][:, None]).min(axis=0)
+    hi = (centers[small] + radii[small][:, None]).max(axis=0)
+    ext = float((hi - lo).max())
+    pad = 1e-3 * ext + 1e-3  # hit points nudged off the spheres (1e-4) and off a ground they rest on
+    lo, hi = lo - pad, hi + pad
+    cell = (ext + 2 * pad) / SHGRID_CELLS
+    dims = np.maximum(np.ceil((hi - lo) / cell), 1).astype(np.int64)
+    if int(np.prod(dims)) > SHGRID_MAX_VOXELS:
+        return blob
+    inv = 1.0 / cell
+    # voxel boxes (grown by a rounding margin: the kernel's index arithmetic may place q one voxel off
+    # at a boundary)
+    ix, iy, iz = np.meshgrid(np.arange(dims[0]), np.arange(dims[1]), np.arange(dims[2]), indexing="ij")
+    idx = np.stack([ix.ravel(order="F"), iy.ravel(order="F"), iz.ravel(order="F")], axis=1)  # x fastest
+    vlo = lo + idx * cell
+    vhi = lo + (idx + 1) * cell
+    m = (vlo + vhi) * 0.5
+    grow = 1e-9 * (np.abs(lo).max() + np.abs(hi).max() + ext) + 1e-12
+    eps_n = 2e-4
+    rho = np.sqrt(((vhi - vlo) ** 2).sum(axis=1)) * 0.5 * (1 + 1e-12) + grow + eps_n
+    mv = m - light
+    D = np.sqrt((mv ** 2).sum(axis=1))
+    wide = D <= rho * (1 + 1e-9) * 1.01  # the voxel (nearly) holds the light: every sphere
+    Ds = np.where(wide, 1.0, D)
+    a = mv / Ds[:, None]
+    sinT = np.minimum(rho / Ds * (1 + 1e-12), 1.0)
+    cosT = np.sqrt(np.maximum(1.0 - sinT * sinT, 0.0)) * (1 - 1e-12)
+    w = centers - light  # [S, 3]
+    h = np.abs(a @ w.T)  # [V, S]
+    cr = np.cross(a[:, None, :], w[None, :, :])
+    dperp = np.sqrt((cr ** 2).sum(axis=2))
+    dist = dperp * cosT[:, None] - h * sinT[:, None]
+    qmax = np.sqrt((m ** 2).sum(axis=1)) + rho  # |q| bound per voxel
+    cmag = np.sqrt((centers ** 2).sum(axis=1))
+    wmag = np.sqrt((w ** 2).sum(axis=1))
+    margin = (radii[None, :] * (1 + 1e-12) + 1e-6 * (qmax[:, None] + cmag[None, :] + radii[None, :] + 1.0)
+              + eps_n + 1e-9 * (wmag[None, :] + D[:, None] + rho[:, None]))
+    may = ~(dist > margin) | wide[:, None]
+    bits = np.zeros((may.shape[0], 2), dtype=np.uint64)
+    for j in range(S):
+        bits[may[:, j], j >> 6] |= np.uint64(1) << np.uint64(j & 63)
+    rec = np.concatenate([lo, [inv, inv, inv], dims.astype(np.float64), bits.view(np.float64).ravel()])
+    off = blob.size
+    out = np.concatenate([blob, rec])
+    out[L.H_SHGRID] = off
     return out
 
 

@@ -419,3 +419,51 @@ def test_pack_override_material():
     off = int(blob[L.H_MAT0])
     assert blob[off + L.M_TEX] == L.TEX_IMAGE and int(blob[off + L.M_TR]) == off + L.MAT_WORDS
     assert np.array_equal(blob[off + L.MAT_WORDS:].reshape(4, 6, 3), img / 255.0)
+
+
+@pytest.mark.parametrize("n_spheres,light", [(64, None), (16, [1.5, 2.0, 6.0]), (40, [0.3, 0.6, 8.0])])
+def test_shadow_grid_masks_are_conservative(n_spheres, light):
+    """scene_pack's shadow grid (RTX_H_SHGRID): for hit points sampled on every sphere's surface and
+    on the ground, any sphere the reference's shadow test (shader.py:126-128, oracle.intersect from
+    the nudged point along L_dir) reports as hit must be in the mask of the voxel holding the nudged
+    point, looked up as the kernel does (rtx_kernels.hip grid_mask)."""
+    spec = scenes.random_spec(n_spheres, 7, 64, 36)
+    if light is not None:
+        spec["lights"][0]["position"] = light
+    sc = O.scene_from_spec(spec)
+    blob = scene_pack.pack_scene(scenes.build_scene(spec))
+    off = int(blob[L.H_SHGRID])
+    assert off > 0
+    g = blob[off:off + L.SHGRID_WORDS]
+    nx, ny, nz = (int(v) for v in g[6:9])
+    masks = blob[off + L.SHGRID_WORDS: off + L.SHGRID_WORDS + 2 * nx * ny * nz].view(np.uint64).reshape(-1, 2)
+    rng = np.random.default_rng(11)
+    lx0, ly0, lz0 = sc.light_pos
+    checked = 0
+    for si, sp in enumerate(sc.spheres):
+        m = 4000 if sp.radius > 100 else 400
+        if sp.radius > 100:  # the ground near the spheres: points under the grid's x/z extent
+            x = rng.uniform(g[0], g[0] + nx / g[3], m)
+            z = rng.uniform(g[2], g[2] + nz / g[5], m)
+            y = sp.cy + np.sqrt(sp.radius ** 2 - (x - sp.cx) ** 2 - (z - sp.cz) ** 2)
+            u = np.stack([(x - sp.cx) / sp.radius, (y - sp.cy) / sp.radius, (z - sp.cz) / sp.radius])
+        else:
+            u = rng.normal(size=(3, m))
+            u /= np.sqrt((u ** 2).sum(axis=0))
+        px, py, pz = sp.cx + sp.radius * u[0], sp.cy + sp.radius * u[1], sp.cz + sp.radius * u[2]
+        inv_r = 1.0 / sp.radius
+        nxv, nyv, nzv = (px - sp.cx) * inv_r, (py - sp.cy) * inv_r, (pz - sp.cz) * inv_r
+        lx, ly, lz = O._norm(lx0 - px, ly0 - py, lz0 - pz)
+        qx, qy, qz = px + nxv * 0.0001, py + nyv * 0.0001, pz + nzv * 0.0001
+        fx, fy, fz = (qx - g[0]) * g[3], (qy - g[1]) * g[4], (qz - g[2]) * g[5]
+        inside = (fx >= 0) & (fx < nx) & (fy >= 0) & (fy < ny) & (fz >= 0) & (fz < nz)
+        key = (fz.astype(np.int64) * ny + fy.astype(np.int64)) * nx + fx.astype(np.int64)
+        for j, other in enumerate(sc.spheres):
+            t = O.intersect(other, qx, qy, qz, lx, ly, lz)
+            hit = inside & (t < O.FARAWAY)
+            if not hit.any():
+                continue
+            bits = masks[key[hit], j >> 6] >> np.uint64(j & 63) & np.uint64(1)
+            assert bits.all(), (si, j, int((bits == 0).sum()))
+            checked += int(hit.sum())
+    assert checked > 1000
