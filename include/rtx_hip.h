@@ -94,12 +94,14 @@ enum {
                         reflections through the unchanged scene, :152); 0 = none */
   RTX_H_SHGRID = 39  /* optional shadow grid (scenes with a culling tree and at most 128 spheres): word
                         offset of its record, 0 = none. Record: lo x,y,z; 1/cell x,y,z; nx, ny, nz;
-                        then per voxel (x fastest) two 64-bit masks stored as the bits of two doubles:
-                        bit j of mask k set unless sphere 64k+j provably cannot shadow (shader.py:126-128
-                        in its any-hit form) a shadow ray whose nudged origin lies in the voxel */
+                        centre x,y,z and grown radius of the small spheres' bounding ball; then per
+                        voxel (x fastest) two 64-bit masks stored as the bits of two doubles: bit j of
+                        mask k set unless sphere 64k+j provably cannot shadow (shader.py:126-128 in its
+                        any-hit form) a shadow ray whose nudged origin lies in the voxel; last, the
+                        huge spheres' mask (rays outside the grid that miss the ball) */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
-#define RTX_SHGRID_WORDS 9  /* words of the shadow-grid record before its masks */
+#define RTX_SHGRID_WORDS 13 /* words of the shadow-grid record before its masks */
 
 /* per-sphere geometry words */
 enum {

@@ -960,41 +960,57 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
 }
 
 // ---- shadow grid (RTX_H_SHGRID, scene_pack._append_shadow_grid) ---------------------------
-// The union, over the wave's lanes, of the voxel masks of their nudged hit points q: the spheres
-// that may shadow any of them. False (use the culling tree) when some lane's q lies outside the
-// grid, has |N|^2 > 4 (the grid's nudge bound) or is NaN, or when the lanes span more than
-// kGridWaterfall voxels.
+// The union, over the wave's lanes, of the masks of their shadow rays (origin q, direction L_dir):
+// a lane whose q lies in the grid takes its voxel's mask (the spheres that may shadow any point of
+// it); a lane outside takes the huge spheres' mask if its ray's line passes the small spheres'
+// bounding ball at more than its radius plus the rounding reach (distance^2 from the centre: |w|^2 -
+// (w.L_dir)^2, whose rounding, <= 4.4e-16 |w|^2, the 3e-8 (|w|^2 + 1) term covers; the host grows
+// the radius by 1e-6 (|Cb| + Rb + 1), the lane adds 1e-6 |q| <= 5e-7 (|q|^2 + 1)). The wave-uniform
+// own shape hs is removed. False (use the culling tree or the linear loop) when some lane fails
+// both, has |N|^2 > 4 (the voxel masks' nudge bound) or NaNs, or when the lanes span more than
+// kGridWaterfall distinct masks.
 constexpr int kGridWaterfall = 8;
-__device__ __forceinline__ bool grid_mask(const cdouble* sc, double qx, double qy, double qz, double n2, uint64_t& m0,
-                                          uint64_t& m1) {
+__device__ __forceinline__ bool grid_mask(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
+                                          double ly, double lz, double n2, int hs, uint64_t& m0, uint64_t& m1) {
   const cdouble* gr = sc + (int)sc[RTX_H_SHGRID];
   const double fx = (qx - gr[0]) * gr[3], fy = (qy - gr[1]) * gr[4], fz = (qz - gr[2]) * gr[5];
   const bool in = fx >= 0.0 && fx < gr[6] && fy >= 0.0 && fy < gr[7] && fz >= 0.0 && fz < gr[8] && n2 <= 4.0;
-  if (__ballot(!in) != 0) return false;
-  const int key = ((int)fz * (int)gr[7] + (int)fy) * (int)gr[6] + (int)fx;
+  const int nx = (int)gr[6], ny = (int)gr[7];
+  int key = ((int)fz * ny + (int)fy) * nx + (int)fx;
+  bool ok = in;
+  if (!in) {
+    const double wx = gr[9] - qx, wy = gr[10] - qy, wz = gr[11] - qz;
+    const double ww = (wx * wx + wy * wy) + wz * wz;
+    const double hh = (wx * lx + wy * ly) + wz * lz;
+    const double R = (gr[12] + 5e-7 * (qq + 1.0)) + 3e-8 * (ww + 1.0);
+    ok = ww - hh * hh > R * R;
+    key = nx * ny * (int)gr[8];  // the huge spheres' mask
+  }
+  if (__ballot(!ok) != 0) return false;
   const cdouble* masks = gr + RTX_SHGRID_WORDS;
   m0 = 0;
   m1 = 0;
   bool pend = true;
   for (int it = 0;; ++it) {
     const uint64_t b = __ballot(pend);
-    if (b == 0) return true;
+    if (b == 0) break;
     if (it == kGridWaterfall) return false;
     const int k0 = __builtin_amdgcn_readlane(key, (int)__builtin_ctzll(b));
     m0 |= (uint64_t)__double_as_longlong(masks[2 * k0]);
     m1 |= (uint64_t)__double_as_longlong(masks[2 * k0 + 1]);
     pend = pend && key != k0;
   }
-}
-
-// Shadow any-hit over the candidate spheres of masks m0/m1 (scene order, pairs), skipping the
-// wave-uniform own shape hs: lit stays true unless some candidate is strictly nearer than t_self.
-template <typename G, typename Wk>
-__device__ __forceinline__ bool lit_masked(const G* geo, uint64_t m0, uint64_t m1, int hs, double qx, double qy,
-                                           double qz, double qq, double lx, double ly, double lz, double tself,
-                                           double tame, Wk& wk) {
   if (hs < 64) m0 &= ~(uint64_t(1) << hs);
   else if (hs < 128) m1 &= ~(uint64_t(1) << (hs - 64));
+  return true;
+}
+
+// Shadow any-hit over the candidate spheres of masks m0/m1 (scene order, pairs): lit stays true
+// unless some candidate is strictly nearer than t_self.
+template <typename G, typename Wk>
+__device__ __forceinline__ bool lit_masked(const G* geo, uint64_t m0, uint64_t m1, double qx, double qy, double qz,
+                                           double qq, double lx, double ly, double lz, double tself, double tame,
+                                           Wk& wk) {
   wk.test(__builtin_popcountll(m0) + __builtin_popcountll(m1));
   bool lit = true;
   for (int half = 0; half < 2; ++half) {
@@ -1046,52 +1062,59 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   // _calculate_shadow (:114-128): lit == (t_self == min_j t_j), no light-distance cutoff.
   // Equivalent any-hit form: lit unless some sphere is strictly nearer than the shape itself.
   const double qq = dot3(qx, qy, qz, qx, qy, qz);
-  const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
-  wk.test(1);
-  bool lit = true;
-  // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
-  // shadows. The linear loop handles it exactly; the culling tree skips missing spheres, so such
-  // a wave takes the linear loop.
-  const bool far_self = tself > FARAWAY;
   // The shape's own test is t_self itself (same expression), and t_self < t_self never holds: when
   // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
   const int h0 = __builtin_amdgcn_readfirstlane(h);
   const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
-  const bool culled = TREE && sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
-  if (culled) {
-    uint64_t m0, m1;
-    if (sc[RTX_H_SHGRID] != 0.0 && grid_mask(sc, qx, qy, qz, dot3(nx, ny, nz, nx, ny, nz), m0, m1)) {
-      wk.node();  // the voxel lookup, priced as one node test
-      lit = lit_masked(geo, m0, m1, hs, qx, qy, qz, qq, lx, ly, lz, tself, tame, wk);
-    } else {
-      lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
+  bool lit = true;
+  uint64_t m0, m1;
+  // The shadow grid (tame scenes: t_self < 2^62 < FARAWAY, so no lane is far_self): only the
+  // candidate occluders are tested, and t_self only if there is one (with none, t_self is the
+  // minimum whatever it is: lit). Scenes with a culling tree only: below kTreeMinSpheres the linear
+  // loop is as cheap as the lookup (A/B: C2 +0.7%, C2main +2.7%, C1 +5% with the grid).
+  if (TREE && sc[RTX_H_SHGRID] != 0.0 && sc[RTX_H_TAME] != 0.0 &&
+      grid_mask(sc, qx, qy, qz, qq, lx, ly, lz, dot3(nx, ny, nz, nx, ny, nz), hs, m0, m1)) {
+    wk.node();  // the voxel lookup, priced as one node test
+    if ((m0 | m1) != 0) {
+      const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
+      wk.test(1);
+      lit = lit_masked(geo, m0, m1, qx, qy, qz, qq, lx, ly, lz, tself, tame, wk);
     }
-  }
-  const int nshadow = culled ? 0 : nsph - (hs < nsph);
-  int j = 0;
-  for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
-    const int j0 = __builtin_amdgcn_readfirstlane(j + (j >= hs));
-    const int j1 = __builtin_amdgcn_readfirstlane(j + 1 + (j + 1 >= hs));
-    const G* g0 = geo + j0 * RTX_GEOM_WORDS;
-    const G* g1 = geo + j1 * RTX_GEOM_WORDS;
-    wk.test(2);
-    bool sh = far_self;  // lanes without a valid root in either test
-    isect_pair(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, tame),
-               [&](double t0, bool v0, double t1, bool v1) {
-                 sh = shadows(v0, t0, tself, far_self) || shadows(v1, t1, tself, far_self);
-               });
-    if (sh) {
-      lit = false;
-      break;
-    }
-  }
-  if (lit && j < nshadow) {
-    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
+  } else {
+    const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
     wk.test(1);
-    bool sh = far_self;
-    isect_one(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame),
-              [&](double t0, bool v0) { sh = shadows(v0, t0, tself, far_self); });
-    if (sh) lit = false;
+    // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
+    // shadows. The linear loop handles it exactly; the culling tree skips missing spheres, so such
+    // a wave takes the linear loop.
+    const bool far_self = tself > FARAWAY;
+    const bool culled = TREE && sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
+    if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
+    const int nshadow = culled ? 0 : nsph - (hs < nsph);
+    int j = 0;
+    for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
+      const int j0 = __builtin_amdgcn_readfirstlane(j + (j >= hs));
+      const int j1 = __builtin_amdgcn_readfirstlane(j + 1 + (j + 1 >= hs));
+      const G* g0 = geo + j0 * RTX_GEOM_WORDS;
+      const G* g1 = geo + j1 * RTX_GEOM_WORDS;
+      wk.test(2);
+      bool sh = far_self;  // lanes without a valid root in either test
+      isect_pair(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, tame),
+                 [&](double t0, bool v0, double t1, bool v1) {
+                   sh = shadows(v0, t0, tself, far_self) || shadows(v1, t1, tself, far_self);
+                 });
+      if (sh) {
+        lit = false;
+        break;
+      }
+    }
+    if (lit && j < nshadow) {
+      const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
+      wk.test(1);
+      bool sh = far_self;
+      isect_one(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame),
+                [&](double t0, bool v0) { sh = shadows(v0, t0, tself, far_self); });
+      if (sh) lit = false;
+    }
   }
 
   const double dli = max0(dot3(nx, ny, nz, lx, ly, lz));  // :138

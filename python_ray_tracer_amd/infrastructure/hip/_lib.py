@@ -49,7 +49,7 @@ H_XSTART, H_XSTEP, H_XSTOP, H_XFIX = 20, 21, 22, 23
 H_YSTART, H_YSTEP, H_YSTOP, H_YFIX = 24, 25, 26, 27
 H_VZ, H_VZ2, H_W, H_H, H_CAMOO = 28, 29, 30, 31, 32
 H_NNODES, H_NALWAYS, H_NODES, H_CGEO, H_TAME, H_MAT0, H_SHGRID = 33, 34, 35, 36, 37, 38, 39
-SHGRID_WORDS = 9
+SHGRID_WORDS = 13
 TAME_BOUND = 2.0 ** 60
 # geometry words
 G_CX, G_CY, G_CZ, G_CC, G_RR, G_INVR, G_C0, G_IDX = 0, 1, 2, 3, 4, 5, 6, 7

@@ -162,7 +162,7 @@ def _pack_static(static: tuple) -> np.ndarray:
     blob[L.HDR_WORDS + S * L.GEOM_WORDS:] = np.asarray(mat_rows, dtype=np.float64).ravel()
     if S >= BVH_MIN_SPHERES:
         blob = _append_culling_tree(blob, geo.copy(), S)
-        if S <= SHGRID_MAX_SPHERES:
+        if S <= SHGRID_MAX_SPHERES:  # (the kernel reads the grid only with a culling tree)
             blob = _append_shadow_grid(blob, geo.copy(), S, lpos)
     # image textures: one float64 RGB texel table per distinct image, after everything else; the
     # material's RTX_M_TR word holds its word offset
@@ -377,14 +377,18 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
 # L_dir = norm(light - p) and tests every sphere. Its line passes through q and, since its direction
 # is that of light - p, through light + (q - p), within 1e-4 |N| of the light. For a voxel V of a grid
 # over the small spheres, every such line with q in V therefore lies within eps_n of the double cone
-# with apex at the light around V's bounding ball grown by eps_n (the kernel only uses the grid when
-# every lane has |N|^2 <= 4, so eps_n = 2e-4). A sphere farther from that cone than its radius plus
-# the reference formula's rounding reach (a root it reports lies within lm <= 1.8e-7 (|C| + |q| + r)
-# of the ball, the same budget as node_may_hit; 1e-6 (... + 1) here) yields FARAWAY on every such
-# ray and cannot shadow: the voxel's mask leaves it out. Distance of a point at w from the light to
-# the double cone of unit axis a and half-angle T: |w x a| cos T - |w.a| sin T (for w outside it).
+# with apex at the light around V's bounding ball grown by eps_n (the kernel only uses the voxel
+# masks when every lane has |N|^2 <= 4, so eps_n = 2e-4). A sphere farther from that cone than its
+# radius plus the reference formula's rounding reach (a root it reports lies within
+# lm <= 1.8e-7 (|C| + |q| + r) of the ball, the budget of node_may_hit; 1e-6 (... + 1) here) yields
+# FARAWAY on every such ray and cannot shadow: the voxel's mask leaves it out. Distance of a point
+# at w from the light to the double cone of unit axis a and half-angle T: |w x a| cos T - |w.a| sin T
+# (for w outside it). Rays from outside the grid whose line misses the small spheres' bounding ball
+# (tested per lane in the kernel) can only be shadowed by the huge spheres: the last mask. The grid
+# covers the small spheres and, for a light above them, their shadow on the plane of their lowest
+# point (where a ground under them is hit), at most 3x their extent.
 SHGRID_MAX_SPHERES = 128
-SHGRID_CELLS = 24  # cells along the grid's longest side (cubic cells)
+SHGRID_CELLS = 32  # cells along the grid's longest side (cubic cells)
 SHGRID_MAX_VOXELS = 1 << 14
 
 
@@ -397,12 +401,20 @@ def _append_shadow_grid(blob: np.ndarray, geo: np.ndarray, S: int, lpos) -> np.n
     small = [i for i in range(S) if not (radii[i] > HUGE_RADIUS or float(np.abs(centers[i]).max()) > 1e4)]
     if not small:
         return blob
-    lo = (centers[small] - radii[small][:, None]).min(axis=0)
-    hi = (centers[small] + radii[small][:, None]).max(axis=0)
-    ext = float((hi - lo).max())
+    slo = (centers[small] - radii[small][:, None]).min(axis=0)
+    shi = (centers[small] + radii[small][:, None]).max(axis=0)
+    ext = float((shi - slo).max())
     pad = 1e-3 * ext + 1e-3  # hit points nudged off the spheres (1e-4) and off a ground they rest on
-    lo, hi = lo - pad, hi + pad
-    cell = (ext + 2 * pad) / SHGRID_CELLS
+    lo, hi = slo - pad, shi + pad
+    if light[1] > hi[1]:  # the small spheres' shadow on the plane y = lo_y, within 3x their extent
+        corners = np.array([[x, y, z] for x in (lo[0], hi[0]) for y in (lo[1], hi[1]) for z in (lo[2], hi[2])])
+        f = (light[1] - lo[1]) / (light[1] - corners[:, 1])
+        proj = light + (corners - light) * f[:, None]
+        mid = (lo + hi) * 0.5
+        for ax in (0, 2):
+            lo[ax] = max(min(lo[ax], proj[:, ax].min()), mid[ax] - 1.5 * (ext + 2 * pad))
+            hi[ax] = min(max(hi[ax], proj[:, ax].max()), mid[ax] + 1.5 * (ext + 2 * pad))
+    cell = float((hi - lo).max()) / SHGRID_CELLS
     dims = np.maximum(np.ceil((hi - lo) / cell), 1).astype(np.int64)
     if int(np.prod(dims)) > SHGRID_MAX_VOXELS:
         return blob
@@ -414,12 +426,12 @@ def _append_shadow_grid(blob: np.ndarray, geo: np.ndarray, S: int, lpos) -> np.n
     vlo = lo + idx * cell
     vhi = lo + (idx + 1) * cell
     m = (vlo + vhi) * 0.5
-    grow = 1e-9 * (np.abs(lo).max() + np.abs(hi).max() + ext) + 1e-12
+    grow = 1e-9 * (np.abs(lo).max() + np.abs(hi).max() + float((hi - lo).max())) + 1e-12
     eps_n = 2e-4
     rho = np.sqrt(((vhi - vlo) ** 2).sum(axis=1)) * 0.5 * (1 + 1e-12) + grow + eps_n
     mv = m - light
     D = np.sqrt((mv ** 2).sum(axis=1))
-    wide = D <= rho * (1 + 1e-9) * 1.01  # the voxel (nearly) holds the light: every sphere
+    wide = D <= rho * 1.01  # the voxel (nearly) holds the light: every sphere
     Ds = np.where(wide, 1.0, D)
     a = mv / Ds[:, None]
     sinT = np.minimum(rho / Ds * (1 + 1e-12), 1.0)
@@ -435,10 +447,15 @@ def _append_shadow_grid(blob: np.ndarray, geo: np.ndarray, S: int, lpos) -> np.n
     margin = (radii[None, :] * (1 + 1e-12) + 1e-6 * (qmax[:, None] + cmag[None, :] + radii[None, :] + 1.0)
               + eps_n + 1e-9 * (wmag[None, :] + D[:, None] + rho[:, None]))
     may = ~(dist > margin) | wide[:, None]
-    bits = np.zeros((may.shape[0], 2), dtype=np.uint64)
+    bits = np.zeros((may.shape[0] + 1, 2), dtype=np.uint64)
     for j in range(S):
-        bits[may[:, j], j >> 6] |= np.uint64(1) << np.uint64(j & 63)
-    rec = np.concatenate([lo, [inv, inv, inv], dims.astype(np.float64), bits.view(np.float64).ravel()])
+        bits[:-1][may[:, j], j >> 6] |= np.uint64(1) << np.uint64(j & 63)
+        if j not in small:  # the huge spheres' mask
+            bits[-1, j >> 6] |= np.uint64(1) << np.uint64(j & 63)
+    cb = (slo + shi) * 0.5
+    rb = float(np.sqrt(((shi - slo) ** 2).sum())) * 0.5
+    rb = rb * (1 + 1e-12) + 1e-6 * (float(np.sqrt((cb ** 2).sum())) + rb + 1.0) + 1e-12
+    rec = np.concatenate([lo, [inv, inv, inv], dims.astype(np.float64), cb, [rb], bits.view(np.float64).ravel()])
     off = blob.size
     out = np.concatenate([blob, rec])
     out[L.H_SHGRID] = off

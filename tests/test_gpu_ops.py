@@ -98,7 +98,7 @@ def test_op_argument_checks(env):
     with pytest.raises(RuntimeError, match="must be Double"):
         torch.ops.rt.render_tile(blob.float(), S, 32, 18, 1, 1, 0, 3, 0, ws)
     with pytest.raises(RuntimeError, match="too short"):
-        torch.ops.rt.render_tile(blob, S + 40, 32, 18, 1, 1, 0, 3, 0, ws)
+        torch.ops.rt.render_tile(blob, S + 1000, 32, 18, 1, 1, 0, 3, 0, ws)
     with pytest.raises(RuntimeError, match="geometry"):
         torch.ops.rt.render_tile(blob, S, 32, 18, 1, 2, 2, 3, 0, ws)
     with pytest.raises(RuntimeError, match="contiguous"):

@@ -421,12 +421,14 @@ def test_pack_override_material():
     assert np.array_equal(blob[off + L.MAT_WORDS:].reshape(4, 6, 3), img / 255.0)
 
 
-@pytest.mark.parametrize("n_spheres,light", [(64, None), (16, [1.5, 2.0, 6.0]), (40, [0.3, 0.6, 8.0])])
+@pytest.mark.parametrize("n_spheres,light", [(64, None), (16, [1.5, 2.0, 6.0]), (40, [0.3, 0.6, 8.0]), (8, None),
+                                             (9, [-1.0, 0.2, 3.0]), (12, [0.0, 0.1, 30.0])])
 def test_shadow_grid_masks_are_conservative(n_spheres, light):
     """scene_pack's shadow grid (RTX_H_SHGRID): for hit points sampled on every sphere's surface and
-    on the ground, any sphere the reference's shadow test (shader.py:126-128, oracle.intersect from
-    the nudged point along L_dir) reports as hit must be in the mask of the voxel holding the nudged
-    point, looked up as the kernel does (rtx_kernels.hip grid_mask)."""
+    on the ground (inside and far outside the grid), any sphere the reference's shadow test
+    (shader.py:126-128: oracle.intersect from the nudged point along L_dir) reports as hit must be in
+    the mask the kernel would pick (rtx_kernels.hip grid_mask): the voxel's when the nudged point lies
+    in the grid, else the huge spheres' when the ray's line misses the small spheres' ball."""
     spec = scenes.random_spec(n_spheres, 7, 64, 36)
     if light is not None:
         spec["lights"][0]["position"] = light
@@ -436,15 +438,17 @@ def test_shadow_grid_masks_are_conservative(n_spheres, light):
     assert off > 0
     g = blob[off:off + L.SHGRID_WORDS]
     nx, ny, nz = (int(v) for v in g[6:9])
-    masks = blob[off + L.SHGRID_WORDS: off + L.SHGRID_WORDS + 2 * nx * ny * nz].view(np.uint64).reshape(-1, 2)
+    nvox = nx * ny * nz
+    masks = blob[off + L.SHGRID_WORDS: off + L.SHGRID_WORDS + 2 * (nvox + 1)].view(np.uint64).reshape(-1, 2)
     rng = np.random.default_rng(11)
     lx0, ly0, lz0 = sc.light_pos
-    checked = 0
+    checked = {"voxel": 0, "outside": 0}
     for si, sp in enumerate(sc.spheres):
-        m = 4000 if sp.radius > 100 else 400
-        if sp.radius > 100:  # the ground near the spheres: points under the grid's x/z extent
-            x = rng.uniform(g[0], g[0] + nx / g[3], m)
-            z = rng.uniform(g[2], g[2] + nz / g[5], m)
+        m = 6000 if sp.radius > 100 else 400
+        if sp.radius > 100:  # the ground: under the grid and up to 3x its extent around it
+            ex, ez = nx / g[3], nz / g[5]
+            x = rng.uniform(g[0] - ex, g[0] + 2 * ex, m)
+            z = rng.uniform(g[2] - ez, g[2] + 2 * ez, m)
             y = sp.cy + np.sqrt(sp.radius ** 2 - (x - sp.cx) ** 2 - (z - sp.cz) ** 2)
             u = np.stack([(x - sp.cx) / sp.radius, (y - sp.cy) / sp.radius, (z - sp.cz) / sp.radius])
         else:
@@ -456,14 +460,25 @@ def test_shadow_grid_masks_are_conservative(n_spheres, light):
         lx, ly, lz = O._norm(lx0 - px, ly0 - py, lz0 - pz)
         qx, qy, qz = px + nxv * 0.0001, py + nyv * 0.0001, pz + nzv * 0.0001
         fx, fy, fz = (qx - g[0]) * g[3], (qy - g[1]) * g[4], (qz - g[2]) * g[5]
-        inside = (fx >= 0) & (fx < nx) & (fy >= 0) & (fy < ny) & (fz >= 0) & (fz < nz)
-        key = (fz.astype(np.int64) * ny + fy.astype(np.int64)) * nx + fx.astype(np.int64)
+        n2 = (nxv * nxv + nyv * nyv) + nzv * nzv
+        inside = (fx >= 0) & (fx < nx) & (fy >= 0) & (fy < ny) & (fz >= 0) & (fz < nz) & (n2 <= 4.0)
+        key = np.where(inside, (np.clip(fz, 0, nz - 1).astype(np.int64) * ny + np.clip(fy, 0, ny - 1).astype(np.int64))
+                       * nx + np.clip(fx, 0, nx - 1).astype(np.int64), nvox)
+        wx, wy, wz = g[9] - qx, g[10] - qy, g[11] - qz
+        ww = (wx * wx + wy * wy) + wz * wz
+        hh = (wx * lx + wy * ly) + wz * lz
+        qq = (qx * qx + qy * qy) + qz * qz
+        R = (g[12] + 5e-7 * (qq + 1.0)) + 3e-8 * (ww + 1.0)
+        usable = inside | (ww - hh * hh > R * R)
         for j, other in enumerate(sc.spheres):
+            if j == si:
+                continue  # the own shape never shadows (t_self < t_self is false)
             t = O.intersect(other, qx, qy, qz, lx, ly, lz)
-            hit = inside & (t < O.FARAWAY)
+            hit = usable & (t < O.FARAWAY)
             if not hit.any():
                 continue
             bits = masks[key[hit], j >> 6] >> np.uint64(j & 63) & np.uint64(1)
             assert bits.all(), (si, j, int((bits == 0).sum()))
-            checked += int(hit.sum())
-    assert checked > 1000
+            checked["voxel"] += int((hit & inside).sum())
+            checked["outside"] += int((hit & ~inside).sum())
+    assert checked["voxel"] > 10, checked
