@@ -376,14 +376,16 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
 # _calculate_shadow (shader.py:114-128) casts, from the nudged hit point q = p + 1e-4 N, a ray along
 # L_dir = norm(light - p) and tests every sphere. Its line passes through q and, since its direction
 # is that of light - p, through light + (q - p), within 1e-4 |N| of the light. For a voxel V of a grid
-# over the small spheres, every such line with q in V therefore lies within eps_n of the double cone
-# with apex at the light around V's bounding ball grown by eps_n (the kernel only uses the voxel
-# masks when every lane has |N|^2 <= 4, so eps_n = 2e-4). A sphere farther from that cone than its
-# radius plus the reference formula's rounding reach (a root it reports lies within
+# over the small spheres, every such ray (s > 0) with q in V therefore lies within eps_n of the ray
+# from p through the light, p in V's bounding ball grown by eps_n (the kernel only uses the voxel
+# masks when every lane has |N|^2 <= 4, so eps_n = 2e-4): within eps_n of the capsule of the segment
+# from the ball's centre to the light (radius: the ball's) or of the single cone beyond the light,
+# apex at the light, around the directions from the ball to the light. A sphere farther from both
+# than its radius plus the reference formula's rounding reach (a root it reports lies within
 # lm <= 1.8e-7 (|C| + |q| + r) of the ball, the budget of node_may_hit; 1e-6 (... + 1) here) yields
-# FARAWAY on every such ray and cannot shadow: the voxel's mask leaves it out. Distance of a point
-# at w from the light to the double cone of unit axis a and half-angle T: |w x a| cos T - |w.a| sin T
-# (for w outside it). Rays from outside the grid whose line misses the small spheres' bounding ball
+# FARAWAY or a root <= 0 on every such ray and cannot shadow: the voxel's mask leaves it out.
+# Distance of a point at w from the light to the cone of unit axis a and half-angle T:
+# |w x a| cos T - (w.a) sin T, or |w| when (w.a) cos T + |w x a| sin T < 0 (behind the apex). Rays from outside the grid whose line misses the small spheres' bounding ball
 # (tested per lane in the kernel) can only be shadowed by the huge spheres: the last mask. The grid
 # covers the small spheres and, for a light above them, their shadow on the plane of their lowest
 # point (where a ground under them is hit), at most 3x their extent.
@@ -429,24 +431,30 @@ def _append_shadow_grid(blob: np.ndarray, geo: np.ndarray, S: int, lpos) -> np.n
     grow = 1e-9 * (np.abs(lo).max() + np.abs(hi).max() + float((hi - lo).max())) + 1e-12
     eps_n = 2e-4
     rho = np.sqrt(((vhi - vlo) ** 2).sum(axis=1)) * 0.5 * (1 + 1e-12) + grow + eps_n
-    mv = m - light
+    mv = light - m  # voxel -> light
     D = np.sqrt((mv ** 2).sum(axis=1))
     wide = D <= rho * 1.01  # the voxel (nearly) holds the light: every sphere
     Ds = np.where(wide, 1.0, D)
-    a = mv / Ds[:, None]
+    a = mv / Ds[:, None]  # the cone's axis, pointing away from the voxel
     sinT = np.minimum(rho / Ds * (1 + 1e-12), 1.0)
     cosT = np.sqrt(np.maximum(1.0 - sinT * sinT, 0.0)) * (1 - 1e-12)
     w = centers - light  # [S, 3]
-    h = np.abs(a @ w.T)  # [V, S]
+    # (1) beyond the light: the single cone of apex `light` and axis a
+    h = a @ w.T  # [V, S]
     cr = np.cross(a[:, None, :], w[None, :, :])
     dperp = np.sqrt((cr ** 2).sum(axis=2))
-    dist = dperp * cosT[:, None] - h * sinT[:, None]
+    wmag = np.sqrt((w ** 2).sum(axis=1))
+    behind_apex = h * cosT[:, None] + dperp * sinT[:, None] < 0.0
+    d_cone = np.where(behind_apex, wmag[None, :], dperp * cosT[:, None] - h * sinT[:, None])
+    # (2) from the voxel to the light: the capsule of the segment [m, light] and radius rho
+    cm = centers[None, :, :] - m[:, None, :]  # [V, S, 3]
+    tt = np.clip((cm * mv[:, None, :]).sum(axis=2) / (Ds * Ds)[:, None], 0.0, 1.0)
+    d_seg = np.sqrt(((cm - tt[:, :, None] * mv[:, None, :]) ** 2).sum(axis=2))
     qmax = np.sqrt((m ** 2).sum(axis=1)) + rho  # |q| bound per voxel
     cmag = np.sqrt((centers ** 2).sum(axis=1))
-    wmag = np.sqrt((w ** 2).sum(axis=1))
     margin = (radii[None, :] * (1 + 1e-12) + 1e-6 * (qmax[:, None] + cmag[None, :] + radii[None, :] + 1.0)
               + eps_n + 1e-9 * (wmag[None, :] + D[:, None] + rho[:, None]))
-    may = ~(dist > margin) | wide[:, None]
+    may = ~((d_cone > margin) & (d_seg > margin + rho[:, None])) | wide[:, None]
     bits = np.zeros((may.shape[0] + 1, 2), dtype=np.uint64)
     for j in range(S):
         bits[:-1][may[:, j], j >> 6] |= np.uint64(1) << np.uint64(j & 63)

@@ -422,7 +422,8 @@ def test_pack_override_material():
 
 
 @pytest.mark.parametrize("n_spheres,light", [(64, None), (16, [1.5, 2.0, 6.0]), (40, [0.3, 0.6, 8.0]), (8, None),
-                                             (9, [-1.0, 0.2, 3.0]), (12, [0.0, 0.1, 30.0])])
+                                             (9, [-1.0, 0.2, 3.0]), (12, [0.0, 0.1, 30.0]),
+                                             (24, [0.5, 0.0, 6.0]), (16, [0.0, -0.4, 3.0])])
 def test_shadow_grid_masks_are_conservative(n_spheres, light):
     """scene_pack's shadow grid (RTX_H_SHGRID): for hit points sampled on every sphere's surface and
     on the ground (inside and far outside the grid), any sphere the reference's shadow test
