@@ -2,7 +2,7 @@
 # End-of-round measurement session on the GPU box: per BASELINE config a bench.py line (CPU
 # baselines included) and a rocprofv3 kernel-trace of the same command, then the PMC passes
 # (FETCH_SIZE, WRITE_SIZE, SQ instruction mix, each its own run) for the configs given in PMC_CFGS.
-# Usage: bash tools/gpu_round_profiles.sh <tag> "<configs>"   (env PMC_CFGS="C2 C3")
+# Usage: bash tools/gpu_round_profiles.sh <tag> "<configs>"   (env PMC_CFGS="C2 C3"; "-" = none)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; CFGS=${2:-"C1 C2 C2main C3 C4 C5"}; PMC=${PMC_CFGS:-"C2 C3"}
@@ -15,6 +15,8 @@ bargs() {
   esac
 }
 steps=()
+[ "$CFGS" = "-" ] && CFGS=""
+[ "$PMC" = "-" ] && PMC=""
 for c in $CFGS; do
   steps+=("bench_$c|300|python bench.py $(bargs $c) --cpu-seconds 10 --json-out @OUT@/bench_$c.json")
   steps+=("rocprof_$c|300|rocprofv3 --kernel-trace --stats --output-format csv -d @OUT@/prof_$c -o run -- python3 bench.py $(bargs $c) --cpu-seconds 0 --no-secondary")
