@@ -11,7 +11,7 @@ for f in "$SRC"/bench_*.json; do
   case $c in C5) w=3; s=20;; C4) w=3; s=30;; C3) w=10; s=100;; *) w=20; s=200;; esac
   if [ -d "$SRC/prof_$c" ]; then
     cp "$SRC/prof_$c/run_kernel_stats.csv" "profiles/${PFX}_${c}_rocprof_kernel_stats.csv"
-    python tools/rocprof_summary.py "$SRC/prof_$c" --warmup $w --steps $s > "profiles/${PFX}_${c}_rocprof_timed_region.txt"
+    python tools/rocprof_summary.py "$SRC/prof_$c" --log "$SRC/rocprof_$c.log" > "profiles/${PFX}_${c}_rocprof_timed_region.txt"
   fi
 done
 ls profiles | grep "^${PFX}_"
