@@ -1267,9 +1267,9 @@ __device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, u
   return true;
 }
 
-// Nearest hit of camera rays over the candidate spheres of masks m0 (spheres 0..63) and m1
-// (64..127), in scene order, pairs at a time like nearest_hit.
-template <typename P, typename Wk>
+// Nearest hit over the candidate spheres of masks m0 (spheres 0..63) and m1 (64..127), in scene
+// order, pairs at a time like nearest_hit. CAM: camera rays (level 0, the host's c).
+template <bool CAM, typename P, typename Wk>
 __device__ __forceinline__ void nearest_masked(const P* geo, uint64_t m0, uint64_t m1, double ox, double oy,
                                                double oz, double dx, double dy, double dz, double& tmin, int& hit,
                                                bool& tie, double tame, Wk& wk) {
@@ -1277,16 +1277,20 @@ __device__ __forceinline__ void nearest_masked(const P* geo, uint64_t m0, uint64
   tmin = FARAWAY;
   hit = -1;
   tie = false;
+  const double oo = CAM ? 0.0 : dot3(ox, oy, oz, ox, oy, oz);
+  auto disc = [&](const P* g) {
+    return CAM ? isect_disc_cam(g, ox, oy, oz, dx, dy, dz, tame) : isect_disc(g, ox, oy, oz, oo, dx, dy, dz, tame);
+  };
   auto run = [&](uint64_t m, int base) {
     while (m) {
       const int s0 = base + __builtin_ctzll(m);
       m &= m - 1;
       const P* g0 = geo + s0 * RTX_GEOM_WORDS;
-      const SphTest a0 = isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame);
+      const SphTest a0 = disc(g0);
       if (m) {
         const int s1 = base + __builtin_ctzll(m);
         m &= m - 1;
-        const SphTest a1 = isect_disc_cam(geo + s1 * RTX_GEOM_WORDS, ox, oy, oz, dx, dy, dz, tame);
+        const SphTest a1 = disc(geo + s1 * RTX_GEOM_WORDS);
         isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
           nearest_update(v0, t0, s0, tmin, hit, tie);
           nearest_update(v1, t1, s1, tmin, hit, tie);
@@ -1298,6 +1302,134 @@ __device__ __forceinline__ void nearest_masked(const P* geo, uint64_t m0, uint64
   };
   run(m0, 0);
   run(m1, 64);
+}
+
+// ---- candidates of a wave's reflected rays (levels >= 1 of tree scenes) --------------------------
+// The wave's active rays (O, D) leave from a ball around the first active lane's origin Oc, of
+// radius rho >= |O - Oc|, in directions within angle theta of that lane's direction A
+// (1 - cos theta >= 1 - D.A in every lane). A point X = O + tD (t > 0) within R' of a centre C puts
+// Oc + tD within R'' = R' + rho of it, so D lies within phi = asin(R'' / |C - Oc|) of W = C - Oc and
+// A within theta + phi: cos(A, W) >= cos(theta + phi) = cos theta cos phi - sin theta sin phi
+// (theta, phi <= 90 degrees). With R' = r + lm (the culling margin of wave_frustum, doubled again:
+// scale over the whole ball, |C - O| <= |W| + rho and |O| <= |Oc| + rho), a sphere failing that
+// test (and not reaching the ball itself) yields FARAWAY for every ray of the wave, so the nearest
+// hit (and the tie flag) over the others is unchanged. rho^2 and 1 - cos theta are bounded by
+// powers of two found by ballots (a binary search over the active lanes' exponents, exact under any
+// exec mask), so no cross-lane arithmetic is needed. Comparisons keep the sphere on NaN.
+// Only the active lanes run here (the bounce loop's lanes leave it one by one), so the spheres are
+// dealt out by rank: the active lane of rank k tests spheres k, k + n, k + 2n (n active lanes), and
+// pass j's ballot holds sphere j n + rank(lane) at the lane's bit. False (take the culling tree)
+// when that needs more than kBeamPasses passes, the beam is wider than 60 degrees, the ball larger
+// than 2^6 or the candidates more than kBeamMaxCand.
+constexpr int kBeamPasses = 3;
+constexpr int kBeamMaxCand = 24;
+struct Beam {
+  uint64_t m[kBeamPasses];  // pass j: candidate bits at the testing lanes' positions
+  uint64_t ex;              // the active lanes
+  int n;                    // their count
+  int passes;
+};
+__device__ __forceinline__ double rfl_d(double x) {
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(x));
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(x));
+  return __hiloint2double(hi, lo);
+}
+// max over the active lanes of v in [lo, hi] (binary search by ballots)
+__device__ __forceinline__ int wave_max_int(int v, int lo, int hi) {
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (__ballot(v >= mid) != 0) {
+      lo = mid;
+    } else {
+      hi = mid - 1;
+    }
+  }
+  return lo;
+}
+// e with x < 2^e for x in [0, 2^hi): exponents below lo report lo; NaN and anything larger hi + 1
+__device__ __forceinline__ int pow2_above(double x, int lo, int hi) {
+  if (!(x < __builtin_ldexp(1.0, hi))) return hi + 1;
+  if (x < __builtin_ldexp(1.0, lo - 1)) return lo;
+  const int e = __builtin_amdgcn_frexp_exp(x);  // x = m 2^e, m in [0.5, 1)
+  return e < lo ? lo : e;
+}
+template <typename T>
+__device__ __forceinline__ bool wave_beam(const T* tab, int nsph, double ox, double oy, double oz, double dx,
+                                          double dy, double dz, Beam& bm) {
+  bm.ex = __ballot(1);
+  bm.n = __builtin_popcountll(bm.ex);
+  bm.passes = (nsph + bm.n - 1) / bm.n;
+  if (bm.passes > kBeamPasses) return false;
+  const double Ox = rfl_d(ox), Oy = rfl_d(oy), Oz = rfl_d(oz);
+  const double Ax = rfl_d(dx), Ay = rfl_d(dy), Az = rfl_d(dz);
+  const double wox = ox - Ox, woy = oy - Oy, woz = oz - Oz;
+  const int er = wave_max_int(pow2_above((wox * wox + woy * woy) + woz * woz, -60, 12), -60, 13);
+  const double omc = 1.0 - ((dx * Ax + dy * Ay) + dz * Az);
+  const int ea = wave_max_int(pow2_above(omc, -60, -1), -60, 0);
+  if (er > 12 || ea > -1) return false;
+  const double rho = __builtin_sqrt(__builtin_ldexp(1.0, er)) * (1.0 + 1e-12);
+  const double ct = 1.0 - __builtin_ldexp(1.0, ea);                                 // <= cos theta
+  const double st = __builtin_sqrt(__builtin_ldexp(1.0, ea + 1)) * (1.0 + 1e-12);   // >= sin theta
+  const double om = __builtin_sqrt((Ox * Ox + Oy * Oy) + Oz * Oz) + rho;          // >= |O|
+  const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm.ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm.ex, 0));
+  auto may = [&](int s) {
+    if (s >= nsph) return false;
+    const T* e = tab + s * RTX_GEOM_WORDS;
+    const double wx = e[RTX_G_CX] - Ox, wy = e[RTX_G_CY] - Oy, wz = e[RTX_G_CZ] - Oz;
+    const double rr = e[RTX_G_RR];
+    const double w = __builtin_sqrt((wx * wx + wy * wy) + wz * wz);
+    const double wr = w + rho;
+    const double lm = 4e-7 * ((((wr * wr + 2.0 * e[RTX_G_CC]) + 3.0 * rr) + om * om) + 1.0);
+    const double R = ((__builtin_sqrt(rr) + lm) + rho) * (1.0 + 1e-12);
+    if (!(w > R)) return true;
+    const double aw = (Ax * wx + Ay * wy) + Az * wz;
+    const double rhs = ct * __builtin_sqrt((w - R) * (w + R)) - st * R;
+    return !(aw < rhs - 1e-9 * ((w + R) + 1.0));
+  };
+  int cand = 0;
+#pragma unroll
+  for (int j = 0; j < kBeamPasses; ++j) {
+    bm.m[j] = j < bm.passes ? __ballot(may(j * bm.n + rank)) : 0ull;
+    cand += __builtin_popcountll(bm.m[j]);
+  }
+  return cand <= kBeamMaxCand;
+}
+
+// Nearest hit over a wave beam's candidates (pass j, bit b: sphere j n + popcount(ex below b)),
+// pairs at a time like nearest_hit; in scene order.
+template <typename P, typename Wk>
+__device__ __forceinline__ void nearest_beam(const P* geo, const Beam& bm, double ox, double oy, double oz,
+                                             double dx, double dy, double dz, double& tmin, int& hit, bool& tie,
+                                             double tame, Wk& wk) {
+  tmin = FARAWAY;
+  hit = -1;
+  tie = false;
+  const double oo = dot3(ox, oy, oz, ox, oy, oz);
+  auto sph = [&](uint64_t& m, int base) {
+    const int b = __builtin_ctzll(m);
+    m &= m - 1;
+    return base + __builtin_popcountll(bm.ex & ((uint64_t(1) << b) - 1));
+  };
+#pragma unroll
+  for (int j = 0; j < kBeamPasses; ++j) {
+    uint64_t m = bm.m[j];
+    wk.test(__builtin_popcountll(m));
+    const int base = j * bm.n;
+    while (m) {
+      const int s0 = sph(m, base);
+      const SphTest a0 = isect_disc(geo + s0 * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz, tame);
+      if (m) {
+        const int s1 = sph(m, base);
+        const SphTest a1 = isect_disc(geo + s1 * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz, tame);
+        isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
+          nearest_update(v0, t0, s0, tmin, hit, tie);
+          nearest_update(v1, t1, s1, tmin, hit, tie);
+        });
+      } else {
+        isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s0, tmin, hit, tie); });
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ void load_ray(const Params& p, int64_t i, double& ox, double& oy, double& oz, double& dx,
@@ -1363,7 +1495,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // overlaps the LDS staging of the scene table. DEEP (caps above 8 or none): chains still alive
 // after B levels are deferred with a resume record, and the continuation mode exists; the capped
 // instantiations compile none of it.
-template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE>
+template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   const cdouble* sc = (const cdouble*)p.scene;
@@ -1455,7 +1587,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
           wk.node();
           wk.node();
         }
-        nearest_masked(geo, fm0, fm1, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+        nearest_masked<true>(geo, fm0, fm1, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else if (cam0) {
         nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else {
@@ -1593,7 +1725,18 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_wave(st, RTX_S_WTRACE + kb + k + 1);
     }
     if (TREE && sc[RTX_H_NNODES] != 0.0) {
-      nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+      // the wave's beam candidates (tame scenes up to 128 spheres), else the culling tree
+      Beam bm;
+      const double* btab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
+      if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(btab, nsph, ox, oy, oz, dx, dy, dz, bm)) {
+        for (int j = 0; j < bm.passes; ++j) {  // a lane's sphere test per pass, priced as two node tests
+          wk.node();                            // (like wave_frustum)
+          wk.node();
+        }
+        nearest_beam(geo, bm, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+      } else {
+        nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+      }
     } else if constexpr (LDS) {
       nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     } else {
@@ -1664,6 +1807,9 @@ template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), 
 __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
                                                                    : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   constexpr bool TREE = TP >= 1;
+  // reflected-ray beams (wave_beam): scenes of kPersistMinSpheres and more, capped renders (A/B: C4
+  // -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%)
+  constexpr bool BEAM = TP >= 2 && !DEEP;
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
@@ -1685,7 +1831,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
       for (int64_t t = blockIdx.x; t * kFastBlock < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP, LVL, STATS, TREE>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
     }
@@ -1716,7 +1862,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
     while (k < tiles_c) {
       const int t = c + k * nc;
       const int row = t / p.n_tiles_x;
-      fast_tile<B, LDS, DEEP, LVL, STATS, TREE>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
+      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
       if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
@@ -1730,7 +1876,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
   // spheres, whose pixels run long bounce chains, while sky rows finish at level 0 and so fill the
   // end of the grid (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on
   // the order.
-  fast_tile<B, LDS, DEEP, LVL, STATS, TREE>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
+  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -483,3 +483,86 @@ def test_shadow_grid_masks_are_conservative(n_spheres, light):
             checked["voxel"] += int((hit & inside).sum())
             checked["outside"] += int((hit & ~inside).sum())
     assert checked["voxel"] > 10, checked
+
+
+def _beam_candidates(G, Oc, A, r2, omc, drop_rho=False):
+    """Numpy restatement of rtx_kernels.hip wave_beam for one wave: G = [S, 4] (centre, radius),
+    Oc / A the first active lane's origin / direction, r2 / omc the active lanes' |O - Oc|^2 and
+    1 - D.A. Returns the candidate flags, or None where the kernel falls back to the culling tree."""
+    def p2above(x, lo, hi):
+        e = np.frexp(x)[1]
+        e = np.where(x < 2.0 ** (lo - 1), lo, np.maximum(e, lo))
+        return np.where(~(x < 2.0 ** hi), hi + 1, e)
+
+    er, ea = int(p2above(r2, -60, 12).max()), int(p2above(omc, -60, -1).max())
+    if er > 12 or ea > -1:
+        return None
+    rho = 0.0 if drop_rho else np.sqrt(2.0 ** er) * (1 + 1e-12)
+    ct, st = 1 - 2.0 ** ea, np.sqrt(2.0 ** (ea + 1)) * (1 + 1e-12)
+    om = np.sqrt(Oc @ Oc) + rho
+    Wv = G[:, :3] - Oc
+    w = np.sqrt((Wv ** 2).sum(1))
+    rr, CC = G[:, 3] ** 2, (G[:, :3] ** 2).sum(1)
+    lm = 4e-7 * ((((w + rho) ** 2 + 2 * CC) + 3 * rr) + om * om + 1)
+    R = (np.sqrt(rr) + lm + rho) * (1 + 1e-12)
+    with np.errstate(invalid="ignore"):
+        rhs = ct * np.sqrt((w - R) * (w + R)) - st * R
+    return ~(w > R) | ~(Wv @ A < rhs - 1e-9 * ((w + R) + 1))
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_wave_beam_is_conservative(seed):
+    """The reflected-ray beam cull (rtx_kernels.hip wave_beam, levels >= 1 of scenes of 32 spheres and
+    more): for every 8x8 wave tile and random subsets of its live lanes (the lanes still bouncing), any
+    sphere that the reference's intersect (shape.py:28-51, oracle) reports a hit for on a live lane's
+    reflected ray must be a candidate. Mutation check: without the origin ball's radius rho some
+    wave loses a hit sphere."""
+    spec = scenes.random_spec(64, seed, 160, 96)
+    sc = O.scene_from_spec(spec)
+    W, H = 160, 96
+    G = np.array([[sp.cx, sp.cy, sp.cz, sp.radius] for sp in sc.spheres])
+    dx, dy, dz = O.ray_directions(sc.cam, W, H)
+    ox, oy, oz = (np.full(W * H, c) for c in sc.cam)
+    alive = np.ones(W * H, bool)
+    idx = np.arange(W * H)
+    tile = (idx // W // 8) * (W // 8) + (idx % W) // 8
+    rng = np.random.default_rng(seed)
+    stats = {"waves": 0, "hits": 0, "mutant_misses": 0}
+    for level in range(4):
+        dist = np.stack([np.broadcast_to(O.intersect(sp, ox, oy, oz, dx, dy, dz), (W * H,)) for sp in sc.spheres])
+        if level >= 1:
+            for t in np.unique(tile[alive]):
+                lanes = np.nonzero((tile == t) & alive)[0]
+                for sub in (lanes, lanes[rng.random(lanes.size) < 0.5]):
+                    if sub.size == 0:
+                        continue
+                    f = sub[0]
+                    Oc, A = np.array([ox[f], oy[f], oz[f]]), np.array([dx[f], dy[f], dz[f]])
+                    r2 = (ox[sub] - Oc[0]) ** 2 + (oy[sub] - Oc[1]) ** 2 + (oz[sub] - Oc[2]) ** 2
+                    omc = 1.0 - (dx[sub] * A[0] + dy[sub] * A[1] + dz[sub] * A[2])
+                    cand = _beam_candidates(G, Oc, A, r2, omc)
+                    if cand is None:
+                        continue
+                    stats["waves"] += 1
+                    hit = (dist[:, sub] < O.FARAWAY).any(axis=1)
+                    stats["hits"] += int(hit.sum())
+                    assert not (hit & ~cand).any(), (level, t, np.nonzero(hit & ~cand)[0])
+                    mutant = _beam_candidates(G, Oc, A, r2, omc, drop_rho=True)
+                    stats["mutant_misses"] += int((hit & ~mutant).sum())
+        near = dist.min(0)
+        hit_s = np.where(near < O.FARAWAY, dist.argmin(0), -1)
+        nxt = [a.copy() for a in (ox, oy, oz, dx, dy, dz)]
+        nalive = np.zeros_like(alive)
+        for si, sp in enumerate(sc.spheres):
+            ii = np.nonzero(alive & (hit_s == si))[0]
+            if ii.size == 0:
+                continue
+            _, _, lit, _, q, r = O._shade(sc, si, sp, ox[ii], oy[ii], oz[ii], dx[ii], dy[ii], dz[ii], near[ii])
+            j = ii[lit & (sp.specular_gain != 0)]
+            for a, v in zip(nxt, (*q, *r)):
+                a[j] = v[lit & (sp.specular_gain != 0)]
+            nalive[j] = True
+        ox, oy, oz, dx, dy, dz = nxt
+        alive = nalive
+    assert stats["waves"] > 200 and stats["hits"] > 200, stats
+    assert stats["mutant_misses"] > 0, stats

@@ -22,6 +22,25 @@ sys.path.insert(0, str(REPO))
 from python_ray_tracer_amd import _build  # noqa: E402
 
 
+def trim(src: str, caps: set) -> str:
+    """Instantiate only the capped fast kernels of `caps` (timing builds: other caps, unbounded
+    renders and stats buffers then launch nothing)."""
+    def sub(old, new):
+        nonlocal src
+        if old not in src:
+            raise SystemExit(f"--only-b: pattern not found: {old!r}")
+        src = src.replace(old, new)
+
+    for b in range(6):
+        if b not in caps:
+            sub(f"    case {b}: launch_fast_b<{b}>(p, grid, s); break;\n", "")
+    if 6 not in caps:
+        sub("    default: launch_fast_b<6>(p, grid, s); break;", "    default: break;")
+    sub("{ launch_fast_b<kDeepLevels, true>(p, grid, s); }", "{}")
+    sub("    launch_fast_lds_s<B, DEEP, LVL, true>(p, grid, s);", "    launch_fast_lds_s<B, DEEP, LVL, false>(p, grid, s);")
+    return src
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
@@ -29,6 +48,9 @@ def main():
     ap.add_argument("--rev", default=None, help="git revision of csrc/rtx_kernels.hip to build")
     ap.add_argument("--patch", default=None, help="python file defining patch(src) -> src")
     ap.add_argument("--flag", action="append", default=[], help="extra hipcc flag")
+    ap.add_argument("--only-b", default=None,
+                    help="comma list of bounce caps to instantiate (A/B builds in ~1/10 of the time: no "
+                         "other caps, no deep/unbounded kernels, no stats instantiations)")
     a = ap.parse_args()
     rel = _build.SRC.relative_to(REPO)
     if a.rev:
@@ -44,6 +66,8 @@ def main():
             raise SystemExit(f"--set {name}: {n} matching constexpr lines")
     if a.patch:
         src = runpy.run_path(a.patch)["patch"](src)
+    if a.only_b is not None:
+        src = trim(src, {int(b) for b in a.only_b.split(",") if b})
     tmp = _build.SRC.with_name(f"_ab_{Path(a.out).stem}.hip")
     tmp.write_text(src)
     try:
