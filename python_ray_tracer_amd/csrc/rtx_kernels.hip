@@ -870,7 +870,8 @@ template <typename M>
 __device__ __forceinline__ double specular(const M* mh, double g, double nx, double ny, double nz, double lx,
                                            double ly, double lz, double vx, double vy, double vz) {
   double Lx = lx, Ly = ly, Lz = lz;
-  norm3_unit(Lx, Ly, Lz);  // :278 (normalised a second time)
+  norm3_unit(Lx, Ly, Lz);  // :278 (normalised a second time; an ulp of L moves a sharp highlight's
+                           // D by ~2500 ulp: skipping it put main.py's 1080p frame 6e-10 off, r4s2)
   double Vx = vx, Vy = vy, Vz = vz;
   norm3_unit(Vx, Vy, Vz);  // :279 (likewise)
   double Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
@@ -882,6 +883,9 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
     Hz = Hz * rh;
   }
   const double NdotV = clip01(dot3(nx, ny, nz, Vx, Vy, Vz));  // :283
+  // :318 (the select at the end, taken early: a wave whose hits all face away from the camera
+  // skips the rest; A/B C2 -0.2%, C2main -0.5%, C1 -0.8%)
+  if (!(NdotV > 0.0)) return 0.0;
   const double NdotH = clip01(dot3(nx, ny, nz, Hx, Hy, Hz));  // :284
   const double VdotH = clip01(dot3(Vx, Vy, Vz, Hx, Hy, Hz));  // :285
   const double NdotL = clip01(dot3(nx, ny, nz, Lx, Ly, Lz));  // :287
@@ -1079,6 +1083,40 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
       const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
       wk.test(1);
       lit = lit_masked(geo, m0, m1, qx, qy, qz, qq, lx, ly, lz, tself, tame, wk);
+    }
+  } else if (!TREE && sc[RTX_H_TAME] != 0.0) {
+    // Scenes without a culling tree, tame: the other spheres first, and t_self only when some lane
+    // has a valid root (t_self < 2^62 < FARAWAY in a tame scene, so an invalid test never shadows
+    // and a lane without a valid root is lit whatever t_self is). lit <=> no valid root strictly
+    // below t_self <=> !(smallest valid root < t_self); a lane's own shape, tested when the wave's
+    // shapes differ, gives t_self itself, which is not below it.
+    const int nshadow = nsph - (hs < nsph);
+    double tsh = FARAWAY;
+    bool anyv = false;
+    int j = 0;
+    for (; j + 1 < nshadow; j += 2) {  // sphere pairs (one scalar-load wait, two interleaved chains)
+      const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
+      const G* g1 = geo + __builtin_amdgcn_readfirstlane(j + 1 + (j + 1 >= hs)) * RTX_GEOM_WORDS;
+      wk.test(2);
+      isect_pair(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, tame),
+                 [&](double t0, bool v0, double t1, bool v1) {
+                   if (v0) tsh = __builtin_fmin(tsh, t0);
+                   if (v1) tsh = __builtin_fmin(tsh, t1);
+                   anyv = anyv || v0 || v1;
+                 });
+    }
+    if (j < nshadow) {
+      const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;
+      wk.test(1);
+      isect_one(isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame), [&](double t0, bool v0) {
+        if (v0) tsh = __builtin_fmin(tsh, t0);
+        anyv = anyv || v0;
+      });
+    }
+    if (__ballot(anyv) != 0) {
+      const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
+      wk.test(1);
+      lit = !(anyv && tsh < tself);
     }
   } else {
     const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
