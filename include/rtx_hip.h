@@ -92,13 +92,16 @@ enum {
                         replaces the shape's own at level 0 — NumpyShader.create called on another
                         shape's shader (shader.py:63-112 reads self.* for the hit, and traces the
                         reflections through the unchanged scene, :152); 0 = none */
-  RTX_H_SHGRID = 39  /* optional shadow grid (scenes with a culling tree and at most 128 spheres): word
+  RTX_H_SHGRID = 39, /* optional shadow grid (scenes with a culling tree and at most 128 spheres): word
                         offset of its record, 0 = none. Record: lo x,y,z; 1/cell x,y,z; nx, ny, nz;
                         centre x,y,z and grown radius of the small spheres' bounding ball; then per
                         voxel (x fastest) two 64-bit masks stored as the bits of two doubles: bit j of
                         mask k set unless sphere 64k+j provably cannot shadow (shader.py:126-128 in its
                         any-hit form) a shadow ray whose nudged origin lies in the voxel; last, the
                         huge spheres' mask (rays outside the grid that miss the ball) */
+  RTX_H_SINRED = 40  /* 1: every material's thin-film phase (shader.py:208, |phase| <= 10 pi |thickness|)
+                        lies in the kernel sine's reduction range (|x| <= 2^20), so no lane needs a
+                        range check; 0: checked per wave */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 #define RTX_SHGRID_WORDS 13 /* words of the shadow-grid record before its masks */

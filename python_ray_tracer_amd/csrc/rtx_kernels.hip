@@ -765,9 +765,10 @@ __device__ __forceinline__ double sin_reduced(double x) {
   const double s = __builtin_fma(r * z, q, r);
   return ((int)n & 1) ? -s : s;
 }
-__device__ __forceinline__ double sin_ref(double x) {
-  // wave-uniform: the reduction above unless some active lane is out of its range (or NaN / inf)
-  if (__ballot(!(fabs(x) <= 0x1.0p20)) == 0) return sin_reduced(x);
+__device__ __forceinline__ double sin_ref(const cdouble* sc, double x) {
+  // the reduction above when the host bounded every material's phase (RTX_H_SINRED), else
+  // wave-uniform: unless some active lane is out of its range (or NaN / inf)
+  if (sc[RTX_H_SINRED] != 0.0 || __ballot(!(fabs(x) <= 0x1.0p20)) == 0) return sin_reduced(x);
   return sin(x);
 }
 
@@ -948,7 +949,7 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   if (igain != 0.0) {
     const double af = fabs(va - 0.5) * 2.0;  // :204
     const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
-    const double ip = sin_ref(phase);  // :211
+    const double ip = sin_ref(sc, phase);  // :211
     const double hs = mh[RTX_M_HS], omhs = mh[RTX_M_1MHS];
     const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
     const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222

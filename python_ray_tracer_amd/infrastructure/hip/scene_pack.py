@@ -160,6 +160,7 @@ def _pack_static(static: tuple) -> np.ndarray:
     geo = blob[L.HDR_WORDS: L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, L.GEOM_WORDS)
     geo[:] = np.asarray(geo_rows, dtype=np.float64)
     blob[L.HDR_WORDS + S * L.GEOM_WORDS:] = np.asarray(mat_rows, dtype=np.float64).ravel()
+    h[L.H_SINRED] = 1.0 if all(sin_reduced_ok(m) for m in mat_rows) else 0.0
     if S >= BVH_MIN_SPHERES:
         blob = _append_culling_tree(blob, geo.copy(), S)
         if S <= SHGRID_MAX_SPHERES:  # (the kernel reads the grid only with a culling tree)
@@ -216,6 +217,12 @@ def _material_row(fields) -> list:
     return m
 
 
+def sin_reduced_ok(m) -> bool:
+    """RTX_H_SINRED for one material record: its thin-film phase ((af * pi) * thickness) * 10 with
+    af in [0, 1] (shader.py:204-208) stays inside the kernel sine's reduction range (|x| <= 2^20)."""
+    return bool(abs(m[L.M_TFT]) <= L.SIN_TFT_MAX)
+
+
 def pack_override(scene, shape, shader) -> np.ndarray:
     """The blob of ``scene`` plus a level-0 material record for ``shader`` (RTX_H_MAT0):
     NumpyShader.create called on a shader that is not ``shape``'s own shades the hits with the
@@ -236,6 +243,8 @@ def pack_override(scene, shape, shader) -> np.ndarray:
         parts.append(fields[2][1].texels.ravel())
     out = np.concatenate(parts)
     out[L.H_MAT0] = off
+    if not sin_reduced_ok(m):
+        out[L.H_SINRED] = 0.0
     return out
 
 

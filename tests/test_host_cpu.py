@@ -47,6 +47,8 @@ def test_abi_layout_matches_header():
     assert const("RTX_M_TFIOR") == L.M_TFIOR
     assert const("RTX_G_C0") == L.G_C0
     assert const("RTX_H_TAME") == L.H_TAME
+    assert const("RTX_H_SHGRID") == L.H_SHGRID
+    assert const("RTX_H_SINRED") == L.H_SINRED
     assert const("RTX_MAGIC") == L.MAGIC
     assert const("RTX_UNBOUNDED_LEVELS") == L.UNBOUNDED_LEVELS
     lay = (ctypes.c_int * 8)()
@@ -566,3 +568,22 @@ def test_wave_beam_is_conservative(seed):
         alive = nalive
     assert stats["waves"] > 200 and stats["hits"] > 200, stats
     assert stats["mutant_misses"] > 0, stats
+
+
+def test_pack_sin_range_flag():
+    """RTX_H_SINRED: set when every material's thin-film phase (at most 10 pi |thickness|,
+    shader.py:204-208) lies in the kernel sine's reduction range; a thickness beyond it (also on
+    Shader.create's override material) clears it, and the kernel then checks every wave."""
+    from python_ray_tracer_amd.infrastructure.hip import HipShader
+
+    spec = scenes.random_spec(5, 1, 16, 9)
+    assert scene_pack.pack_scene(scenes.build_scene(spec))[L.H_SINRED] == 1.0
+    sc = scenes.build_scene(spec)
+    far = HipShader(0.5, 0.5, 0.5, 0.1, 1.0, sc.shapes[0].shader.diffuse_color)
+    far.thin_film_thickness = 1e5
+    assert scene_pack.pack_override(sc, sc.shapes[1], far)[L.H_SINRED] == 0.0
+    near = HipShader(0.5, 0.5, 0.5, 0.1, 1.0, far.diffuse_color)
+    near.thin_film_thickness = 3e4
+    assert scene_pack.pack_override(sc, sc.shapes[1], near)[L.H_SINRED] == 1.0
+    sc.shapes[2].shader.thin_film_thickness = -1e5
+    assert scene_pack.pack_scene(sc)[L.H_SINRED] == 0.0
