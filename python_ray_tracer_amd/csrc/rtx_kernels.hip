@@ -49,6 +49,10 @@ constexpr int kBlock = 256;   // threads per block of the elementwise boundary k
 // ---- tuning constants (each value chosen by an A/B on identical output, profiles/r1_ab_variants.txt;
 // tools/ab_build.py builds variants by rewriting these lines) ----
 constexpr int kWaveW = 8;       // pixels per wave row: a wave renders a kWaveW x (64 / kWaveW) tile
+// ... in scenes below kTreeMinSpheres (the TREE = false kernels; A/B profiles/r3_ab_variants.txt r3x-r3z:
+// C2 -0.8%, C2main -1.1%, C1 -6%; the culled kernels keep 8 x 8: C5 +0.6%, C4 +3% at 16 x 4, the
+// wave frustum and beam bounds are tighter on square tiles)
+constexpr int kWaveWSmall = 16;
 constexpr int kFastWaves = 4;   // waves per k_render_fast block (1, 2 or 4)
 // k_render_fast single-frame launches of scenes with at least this many spheres: persistent waves
 // fetching wave tiles (A/B: 65 spheres -14%, 17 spheres +-0, 3-16 spheres without the culling tree
@@ -90,8 +94,9 @@ static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "kMaxFetch must be a power of 
 constexpr int kFastBlock = 64 * kFastWaves;
 constexpr int kWavesX = kFastWaves == 1 ? 1 : 2;  // block tile: kWavesX x kWavesY waves
 constexpr int kWavesY = kFastWaves / kWavesX;
-constexpr int kTileW = kWavesX * kWaveW;
-constexpr int kTileH = kWavesY * kWaveH;
+static_assert(kWaveWSmall > 0 && kWaveWSmall <= 64 && 64 % kWaveWSmall == 0, "kWaveWSmall");
+template <bool TREE>
+__host__ __device__ constexpr int wave_w() { return TREE ? kWaveW : kWaveWSmall; }
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kFetchStride = 32;  // uint32 words between counters
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
@@ -1549,11 +1554,12 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const double* rin = nullptr;  // mode 2: the chain's resume record (levels 0..kb-1)
   int col = 0, lr = 0;         // mode 0: the pixel's column and local row
   if (p.mode == 0) {
-    // kWavesX x kWavesY waves per block; wave w -> kWaveW x kWaveH sub-tile, lane -> (l % kWaveW, l / kWaveW)
-    // (wave_tile: (bx, by) is this wave's own kWaveW x kWaveH tile)
+    // kWavesX x kWavesY waves per block; wave w -> WW x WH sub-tile, lane -> (l % WW, l / WW)
+    // (wave_tile: (bx, by) is this wave's own WW x WH tile; TREE only, so WW = kWaveW there)
+    constexpr int WW = wave_w<TREE>(), WH = 64 / WW;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    col = wave_tile ? bx * kWaveW + (lane % kWaveW) : bx * kTileW + (w % kWavesX) * kWaveW + (lane % kWaveW);
-    lr = wave_tile ? by * kWaveH + (lane / kWaveW) : by * kTileH + (w / kWavesX) * kWaveH + (lane / kWaveW);
+    col = wave_tile ? bx * WW + (lane % WW) : bx * (kWavesX * WW) + (w % kWavesX) * WW + (lane % WW);
+    lr = wave_tile ? by * WH + (lane / WW) : by * (kWavesY * WH) + (w / kWavesX) * WH + (lane / WW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else if (!DEEP || p.mode == 1 || p.mode == 3) {
@@ -2472,8 +2478,13 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
     dim3 grid;
-    const int tx = p.mode == 0 ? (p.width + kTileW - 1) / kTileW : (int)((p.n + kFastBlock - 1) / kFastBlock);
-    const int ty = p.mode == 0 ? (p.n_rows + kTileH - 1) / kTileH : 1;
+    // block tiles: the TREE = false kernels (scenes below kTreeMinSpheres, launch_fast_lds_s) use
+    // wave_w<false>() pixels per wave row
+    const bool small = p.nsph < kTreeMinSpheres;
+    const int tw = kWavesX * (small ? wave_w<false>() : wave_w<true>());
+    const int th = kWavesY * (64 / (small ? wave_w<false>() : wave_w<true>()));
+    const int tx = p.mode == 0 ? (p.width + tw - 1) / tw : (int)((p.n + kFastBlock - 1) / kFastBlock);
+    const int ty = p.mode == 0 ? (p.n_rows + th - 1) / th : 1;
     p.n_fetch = 0;
     if (p.nsph >= kPersistMinSpheres && p.mode == 0 && p.n_frames == 1) {
       p.n_tiles_x = (p.width + kWaveW - 1) / kWaveW;  // wave tiles
