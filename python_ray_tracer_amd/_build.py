@@ -11,6 +11,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 SRC = PKG / "csrc" / "rtx_kernels.hip"
+SMALL_SRC = PKG / "csrc" / "rtx_small.hip"  # includes SRC's device code
 HDR = REPO / "include" / "rtx_hip.h"
 LIB = PKG / "librtx_hip.so"
 OPS_SRC = PKG / "csrc" / "rt_ops.cpp"
@@ -18,11 +19,14 @@ OPS_LIB = PKG / "librt_ops.so"
 
 # -ffp-contract=off: NumPy never fuses a*b+c, and FMA contraction would move linspace / checker
 # boundaries. No fast-math: sqrt and division stay correctly rounded.
-HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
                "-Wall", "-Wno-unused-function", "-Wno-unused-result",
                # MachineLICM hoists the ocml sin polynomial constants out of the bounce loop into VGPRs,
                # which then spill at 128 VGPRs; A/B (profiles/r1_ab_variants.txt): faster on every config
                "-mllvm", "-disable-machine-licm"]
+# rtx_small.hip only (the TREE = false kernels): the max-ilp machine scheduler (A/B in
+# profiles/r3_ab_variants.txt: C2 -0.5..-0.9%, C1 -2.4%; the culled kernels lose with it, C4 +1.4%)
+SMALL_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 
 
 def hipcc() -> str:
@@ -36,19 +40,40 @@ def needs_build() -> bool:
     if not LIB.exists():
         return True
     t = LIB.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in (SRC, HDR, Path(__file__)))
+    return any(p.stat().st_mtime > t for p in (SRC, SMALL_SRC, HDR, Path(__file__)))
+
+
+def compile_units(out: Path, main_src: Path, small_src: Path | None, extra_flags=(), verbose: bool = False) -> None:
+    """Compile the library's translation units to objects (in parallel) and link ``out``: main_src
+    with HIPCC_FLAGS, small_src (None: a single-unit source) with SMALL_FLAGS added."""
+    units = [(main_src, [])] + ([(small_src, SMALL_FLAGS)] if small_src is not None else [])
+    objs, procs = [], []
+    for src, flags in units:
+        obj = out.with_name(f"{out.stem}.{src.stem}.o")
+        cmd = [hipcc(), *HIPCC_FLAGS, *flags, *extra_flags, "-c", "-o", str(obj), str(src)]
+        if verbose:
+            print(" ".join(cmd))
+        objs.append(obj)
+        procs.append((subprocess.Popen(cmd, cwd=str(REPO)), cmd))
+    for proc, cmd in procs:
+        if proc.wait() != 0:
+            raise subprocess.CalledProcessError(proc.returncode, cmd)
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *map(str, objs)]
+    if verbose:
+        print(" ".join(cmd))
+    try:
+        subprocess.run(cmd, check=True, cwd=str(REPO))
+    finally:
+        for obj in objs:
+            obj.unlink(missing_ok=True)
 
 
 def build_library(force: bool = False, extra_flags=(), out: Path | None = None, verbose: bool = False) -> Path:
     out = LIB if out is None else Path(out)
     if not force and out == LIB and not needs_build():
         return out
-    cmd = [hipcc(), *HIPCC_FLAGS, *extra_flags, "-o", str(out), str(SRC)]
-    if verbose:
-        print(" ".join(cmd))
     tmp = out.with_suffix(".so.tmp")
-    cmd[-2] = str(tmp)
-    subprocess.run(cmd, check=True, cwd=str(REPO))
+    compile_units(tmp, SRC, SMALL_SRC, extra_flags, verbose)
     os.replace(tmp, out)
     return out
 

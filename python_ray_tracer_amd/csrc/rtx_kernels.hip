@@ -2222,6 +2222,22 @@ __global__ __launch_bounds__(kBlock) void k_assemble_rows(const uint8_t* __restr
   }
 }
 
+}  // namespace
+
+// The TREE = false instantiations of k_render_fast (scenes below kTreeMinSpheres) are compiled and
+// launched by their own translation unit, csrc/rtx_small.hip: it includes the device code above and
+// stops here. It builds with the max-ilp machine scheduler (_build.SMALL_FLAGS), a per-unit flag: it
+// gains the small-scene kernels C2 -0.5..-0.9%, C1 -2.4% and costs the culled kernels C4 +1.4%
+// (profiles/r3_ab_variants.txt r3x-r3z).
+#ifndef RTX_DEVICE_CODE_ONLY
+// Launches k_render_fast<B, true, deep, lvl, stats, 0>(*params) on s (events e0/e1 as
+// hipExtLaunchKernelGGL's); hipErrorInvalidValue, nothing launched, for an instantiation the unit
+// does not carry.
+__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats,
+                                                                  const void* params, dim3 grid, uint32_t lds,
+                                                                  hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+namespace {
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -2233,8 +2249,12 @@ int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
   return code;
 }
 
+thread_local hipError_t g_small_err = hipSuccess;  // a launch rtx_launch_small refused
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = g_small_err;
+  g_small_err = hipSuccess;
   if (e != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
     return RTX_E_LAUNCH;
@@ -2375,9 +2395,9 @@ template <int B, bool DEEP, bool LVL, bool STATS>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
   if (p.n_fetch == 0) {  // one tile per block: the instantiations without the persistent loop
-    if (p.nsph < kTreeMinSpheres) {
-      hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0>), grid, dim3(kFastBlock), (uint32_t)lds, s,
-                            prof_event(0), prof_event(1), 0u, p);
+    if (p.nsph < kTreeMinSpheres) {  // TP 0: the rtx_small.hip unit
+      const hipError_t e = rtx_launch_small(B, DEEP, LVL, STATS, &p, grid, (uint32_t)lds, s, prof_event(0), prof_event(1));
+      if (e != hipSuccess) g_small_err = e;
     } else {
       hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 1>), grid, dim3(kFastBlock), (uint32_t)lds, s,
                             prof_event(0), prof_event(1), 0u, p);
@@ -2795,3 +2815,5 @@ int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts,
 }
 
 }  // extern "C"
+
+#endif  // RTX_DEVICE_CODE_ONLY

@@ -70,13 +70,23 @@ def main():
         src = trim(src, {int(b) for b in a.only_b.split(",") if b})
     tmp = _build.SRC.with_name(f"_ab_{Path(a.out).stem}.hip")
     tmp.write_text(src)
+    # sources split in two units (RTX_DEVICE_CODE_ONLY: rtx_small.hip includes the kernel file) get
+    # the small unit too, including the variant's text; older single-unit revisions build alone
+    small = None
+    if "RTX_DEVICE_CODE_ONLY" in src:
+        small_src = (subprocess.run(["git", "show", f"{a.rev}:{_build.SMALL_SRC.relative_to(REPO)}"], cwd=REPO,
+                                    check=True, capture_output=True, text=True).stdout
+                     if a.rev else _build.SMALL_SRC.read_text())
+        small = _build.SRC.with_name(f"_ab_{Path(a.out).stem}_small.hip")
+        small.write_text(small_src.replace('#include "rtx_kernels.hip"', f'#include "{tmp.name}"'))
     try:
         out = Path(a.out).resolve()
         out.parent.mkdir(parents=True, exist_ok=True)
-        cmd = [_build.hipcc(), *_build.HIPCC_FLAGS, *a.flag, "-o", str(out), str(tmp)]
-        subprocess.run(cmd, check=True, cwd=str(REPO))
+        _build.compile_units(out, tmp, small, a.flag)
     finally:
         tmp.unlink(missing_ok=True)
+        if small is not None:
+            small.unlink(missing_ok=True)
     print(out)
 
 
