@@ -43,10 +43,12 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in (SRC, SMALL_SRC, HDR, Path(__file__)))
 
 
-def compile_units(out: Path, main_src: Path, small_src: Path | None, extra_flags=(), verbose: bool = False) -> None:
+def compile_units(out: Path, main_src: Path, small_src: Path | None, extra_flags=(), verbose: bool = False,
+                  small_flags=None) -> None:
     """Compile the library's translation units to objects (in parallel) and link ``out``: main_src
-    with HIPCC_FLAGS, small_src (None: a single-unit source) with SMALL_FLAGS added."""
-    units = [(main_src, [])] + ([(small_src, SMALL_FLAGS)] if small_src is not None else [])
+    with HIPCC_FLAGS, small_src (None: a single-unit source) with SMALL_FLAGS (or small_flags) added."""
+    sf = list(SMALL_FLAGS if small_flags is None else small_flags)
+    units = [(main_src, [])] + ([(small_src, sf)] if small_src is not None else [])
     objs, procs = [], []
     for src, flags in units:
         obj = out.with_name(f"{out.stem}.{src.stem}.o")

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--rev", default=None, help="git revision of csrc/rtx_kernels.hip to build")
     ap.add_argument("--patch", default=None, help="python file defining patch(src) -> src")
     ap.add_argument("--flag", action="append", default=[], help="extra hipcc flag")
+    ap.add_argument("--small-flag", action="append", default=None,
+                    help="hipcc flag of the small-scene unit only (replaces _build.SMALL_FLAGS)")
     ap.add_argument("--only-b", default=None,
                     help="comma list of bounce caps to instantiate (A/B builds in ~1/10 of the time: no "
                          "other caps, no deep/unbounded kernels, no stats instantiations)")
@@ -82,7 +84,7 @@ def main():
     try:
         out = Path(a.out).resolve()
         out.parent.mkdir(parents=True, exist_ok=True)
-        _build.compile_units(out, tmp, small, a.flag)
+        _build.compile_units(out, tmp, small, a.flag, small_flags=a.small_flag)
     finally:
         tmp.unlink(missing_ok=True)
         if small is not None:
