@@ -32,6 +32,25 @@ def test_library_exports_every_header_symbol():
         assert ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
 
 
+def test_library_links_both_units():
+    """librtx_hip.so is two translation units (csrc/rtx_kernels.hip + csrc/rtx_small.hip, the
+    small-scene kernels): the launch entry of the small unit is defined inside the library (a
+    one-unit build would leave it undefined, found only at the first small-scene render) and hidden."""
+    L.load()
+    so = str(REPO / "python_ray_tracer_amd" / "librtx_hip.so")
+    import shutil
+
+    nm = shutil.which("nm") or shutil.which("llvm-nm")
+    if nm is None:
+        pytest.skip("no nm on PATH")
+    undefined = subprocess.run([nm, "-D", "--undefined-only", so], check=True, capture_output=True, text=True).stdout
+    assert "rtx_launch_small" not in undefined
+    local = subprocess.run([nm, "-C", so], check=True, capture_output=True, text=True).stdout
+    assert re.search(r"^\w+ t rtx_launch_small\(", local, re.M), "rtx_launch_small: not a hidden definition"
+    dynamic = subprocess.run([nm, "-D", so], check=True, capture_output=True, text=True).stdout
+    assert "rtx_launch_small" not in dynamic
+
+
 def test_abi_layout_matches_header():
     text = (REPO / "include" / "rtx_hip.h").read_text()
 
