@@ -93,10 +93,13 @@ static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves
 static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "kMaxFetch must be a power of two");
 constexpr int kFastBlock = 64 * kFastWaves;
 constexpr int kWavesX = kFastWaves == 1 ? 1 : 2;  // block tile: kWavesX x kWavesY waves
-constexpr int kWavesY = kFastWaves / kWavesX;
+constexpr int kWavesXTree = kFastWaves;  // ... of the culled kernels: one row of waves (A/B r3o: C5 -3.0%, C3 +-0.3%; C1 +9% for the small ones)
 static_assert(kWaveWSmall > 0 && kWaveWSmall <= 64 && 64 % kWaveWSmall == 0, "kWaveWSmall");
 template <bool TREE>
 __host__ __device__ constexpr int wave_w() { return TREE ? kWaveW : kWaveWSmall; }
+template <bool TREE>
+__host__ __device__ constexpr int waves_x() { return TREE ? kWavesXTree : kWavesX; }
+static_assert(kFastWaves % kWavesX == 0 && kFastWaves % kWavesXTree == 0, "block wave layout");
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kFetchStride = 32;  // uint32 words between counters
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
@@ -1554,12 +1557,12 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const double* rin = nullptr;  // mode 2: the chain's resume record (levels 0..kb-1)
   int col = 0, lr = 0;         // mode 0: the pixel's column and local row
   if (p.mode == 0) {
-    // kWavesX x kWavesY waves per block; wave w -> WW x WH sub-tile, lane -> (l % WW, l / WW)
+    // WX x WY waves per block; wave w -> WW x WH sub-tile, lane -> (l % WW, l / WW)
     // (wave_tile: (bx, by) is this wave's own WW x WH tile; TREE only, so WW = kWaveW there)
-    constexpr int WW = wave_w<TREE>(), WH = 64 / WW;
+    constexpr int WW = wave_w<TREE>(), WH = 64 / WW, WX = waves_x<TREE>(), WY = kFastWaves / WX;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    col = wave_tile ? bx * WW + (lane % WW) : bx * (kWavesX * WW) + (w % kWavesX) * WW + (lane % WW);
-    lr = wave_tile ? by * WH + (lane / WW) : by * (kWavesY * WH) + (w / kWavesX) * WH + (lane / WW);
+    col = wave_tile ? bx * WW + (lane % WW) : bx * (WX * WW) + (w % WX) * WW + (lane % WW);
+    lr = wave_tile ? by * WH + (lane / WW) : by * (WY * WH) + (w / WX) * WH + (lane / WW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else if (!DEEP || p.mode == 1 || p.mode == 3) {
@@ -2501,8 +2504,9 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     // block tiles: the TREE = false kernels (scenes below kTreeMinSpheres, launch_fast_lds_s) use
     // wave_w<false>() pixels per wave row
     const bool small = p.nsph < kTreeMinSpheres;
-    const int tw = kWavesX * (small ? wave_w<false>() : wave_w<true>());
-    const int th = kWavesY * (64 / (small ? wave_w<false>() : wave_w<true>()));
+    const int wx = small ? waves_x<false>() : waves_x<true>();
+    const int tw = wx * (small ? wave_w<false>() : wave_w<true>());
+    const int th = (kFastWaves / wx) * (64 / (small ? wave_w<false>() : wave_w<true>()));
     const int tx = p.mode == 0 ? (p.width + tw - 1) / tw : (int)((p.n + kFastBlock - 1) / kFastBlock);
     const int ty = p.mode == 0 ? (p.n_rows + th - 1) / th : 1;
     p.n_fetch = 0;
