@@ -204,8 +204,9 @@ enum {
   RTX_WS_HDR_BYTES = 256
 };
 /* RTX_ST_BAD_SCENE: the scene blob's magic or sphere count (RTX_H_NSPH) disagrees with the
- * n_spheres argument; nothing was rendered. */
-enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2, RTX_ST_BAD_SCENE = 4 };
+ * n_spheres argument; nothing was rendered. RTX_ST_UNRENDERED: a render passed RTX_F_NO_GENERAL
+ * but deferred rays (a tie, an image-textured hit): those pixels were left unwritten. */
+enum { RTX_ST_STACK_OVERFLOW = 1, RTX_ST_LIST_OVERFLOW = 2, RTX_ST_BAD_SCENE = 4, RTX_ST_UNRENDERED = 8 };
 
 enum {
   RTX_OK = 0,
@@ -242,8 +243,9 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
  *  - flags RTX_F_NO_GENERAL: for a capped render (0 <= max_bounces <= RTX_FAST_MAX_BOUNCES) whose
  *    identical earlier launch (same blob content, tile, cap) deferred no ray, the general kernel is
  *    not launched (the render is deterministic, so it defers none again). Passing it for a render
- *    that does defer rays leaves those pixels unwritten and the workspace counters non-zero: the
- *    caller guarantees it. Uncapped renders ignore it. */
+ *    that does defer rays leaves those pixels unwritten and raises the sticky RTX_ST_UNRENDERED
+ *    flag (the workspace counters stay clean, so later calls are unaffected). Uncapped renders
+ *    ignore it. */
 #define RTX_F_NO_GENERAL 1u
 int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int height,
                          int row_block, int n_parts, int part, int n_local_rows,

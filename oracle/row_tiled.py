@@ -56,7 +56,10 @@ def _worker(rank, world, port, spec, B, frames, outfile, row_block, sub):
     from python_ray_tracer_amd import scenes, tiling
     from python_ray_tracer_amd.application import render_frame_distributed
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+
+    # a bound on every gloo rendezvous and collective: a sibling that died cannot hold this one
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
     try:
         if os.environ.get("ROW_TILED_STALL_RANK") == str(rank):  # test hook: a stuck worker (tests/)
             time.sleep(3600)
@@ -110,8 +113,19 @@ def time_row_tiled(spec: dict, max_bounces, procs: int, frames: int = 3, row_blo
                   for r in range(procs)]
             for p in ps:
                 p.start()
-            for p in ps:
-                p.join()
+            # poll: when one worker fails, the others would wait in the gloo rendezvous or the
+            # gather until gloo's own timeout, so they are terminated at once
+            try:
+                while any(p.is_alive() for p in ps):
+                    if any(p.exitcode not in (None, 0) for p in ps):
+                        break
+                    time.sleep(0.05)
+            finally:
+                for p in ps:
+                    if p.is_alive():
+                        p.terminate()
+                for p in ps:
+                    p.join()
             bad = [(r, p.exitcode) for r, p in enumerate(ps) if p.exitcode != 0]
             if bad:
                 raise RuntimeError(f"row-tiled workers failed (rank, exit code): {bad}")

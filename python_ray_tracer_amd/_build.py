@@ -47,36 +47,45 @@ def compile_units(out: Path, main_src: Path, small_src: Path | None, extra_flags
                   small_flags=None) -> None:
     """Compile the library's translation units to objects (in parallel) and link ``out``: main_src
     with HIPCC_FLAGS, small_src (None: a single-unit source) with SMALL_FLAGS (or small_flags) added."""
+    import tempfile
+
     sf = list(SMALL_FLAGS if small_flags is None else small_flags)
     units = [(main_src, [])] + ([(small_src, sf)] if small_src is not None else [])
     objs, procs = [], []
-    for src, flags in units:
-        obj = out.with_name(f"{out.stem}.{src.stem}.o")
-        cmd = [hipcc(), *HIPCC_FLAGS, *flags, *extra_flags, "-c", "-o", str(obj), str(src)]
+    # objects in a directory of this call's own: concurrent builds (several ranks importing on a
+    # fresh checkout) cannot overwrite or delete each other's objects before the link
+    objdir = Path(tempfile.mkdtemp(prefix=f".{out.stem}.", dir=str(out.parent)))
+    try:
+        for src, flags in units:
+            obj = objdir / f"{src.stem}.o"
+            cmd = [hipcc(), *HIPCC_FLAGS, *flags, *extra_flags, "-c", "-o", str(obj), str(src)]
+            if verbose:
+                print(" ".join(cmd))
+            objs.append(obj)
+            procs.append((subprocess.Popen(cmd, cwd=str(REPO)), cmd))
+        for proc, cmd in procs:
+            if proc.wait() != 0:
+                raise subprocess.CalledProcessError(proc.returncode, cmd)
+        cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *map(str, objs)]
         if verbose:
             print(" ".join(cmd))
-        objs.append(obj)
-        procs.append((subprocess.Popen(cmd, cwd=str(REPO)), cmd))
-    for proc, cmd in procs:
-        if proc.wait() != 0:
-            raise subprocess.CalledProcessError(proc.returncode, cmd)
-    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *map(str, objs)]
-    if verbose:
-        print(" ".join(cmd))
-    try:
         subprocess.run(cmd, check=True, cwd=str(REPO))
     finally:
-        for obj in objs:
-            obj.unlink(missing_ok=True)
+        for proc, _ in procs:
+            proc.wait()
+        shutil.rmtree(objdir, ignore_errors=True)
 
 
 def build_library(force: bool = False, extra_flags=(), out: Path | None = None, verbose: bool = False) -> Path:
     out = LIB if out is None else Path(out)
     if not force and out == LIB and not needs_build():
         return out
-    tmp = out.with_suffix(".so.tmp")
-    compile_units(tmp, SRC, SMALL_SRC, extra_flags, verbose)
-    os.replace(tmp, out)
+    tmp = out.with_suffix(f".so.tmp{os.getpid()}")  # per process: concurrent builds each rename a whole file
+    try:
+        compile_units(tmp, SRC, SMALL_SRC, extra_flags, verbose)
+        os.replace(tmp, out)
+    finally:
+        tmp.unlink(missing_ok=True)
     return out
 
 
@@ -101,12 +110,15 @@ def build_ops(force: bool = False, verbose: bool = False) -> Path:
     if not force and OPS_LIB.exists() and all(p.stat().st_mtime <= OPS_LIB.stat().st_mtime
                                               for p in (OPS_SRC, HDR, LIB, Path(__file__))):
         return OPS_LIB
-    tmp = OPS_LIB.with_suffix(".so.tmp")
+    tmp = OPS_LIB.with_suffix(f".so.tmp{os.getpid()}")
     cmd = [hipcc(), "-x", "c++", *ops_flags(), "-o", str(tmp), str(OPS_SRC)]
     if verbose:
         print(" ".join(cmd))
-    subprocess.run(cmd, check=True, cwd=str(REPO))
-    os.replace(tmp, OPS_LIB)
+    try:
+        subprocess.run(cmd, check=True, cwd=str(REPO))
+        os.replace(tmp, OPS_LIB)
+    finally:
+        tmp.unlink(missing_ok=True)
     return OPS_LIB
 
 

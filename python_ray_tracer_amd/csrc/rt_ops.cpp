@@ -22,9 +22,10 @@
 //
 // Error channel of the render ops (render_tile, render_frames, trace, shade_hits), check=True (the
 // default), mirroring HipRenderer:
-//   * before the launch, the scene blob's header (magic, sphere count) is read back to the host —
-//     one small synchronous copy — and a blob that disagrees with n_spheres raises RuntimeError
-//     (the kernel would refuse it, RTX_ST_BAD_SCENE, and render nothing);
+//   * before the first launch on a blob (and again after any in-place write to it), the blob's
+//     header (magic, sphere count) is read back to the host — one small synchronous copy — and a
+//     blob that disagrees with n_spheres raises RuntimeError (the kernel would refuse it,
+//     RTX_ST_BAD_SCENE, and render nothing); later calls on the same blob do not synchronise;
 //   * after a launch that can defer chains beyond the fast kernel's levels (max_bounces -1 or above
 //     RTX_FAST_MAX_BOUNCES), the workspace's status word is read back (a synchronisation) and
 //     cleared; RTX_ST_STACK_OVERFLOW raises RuntimeError("maximum recursion depth exceeded ...",
@@ -36,6 +37,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <mutex>
 #include <vector>
 
 #include "../../include/rtx_hip.h"
@@ -72,9 +74,35 @@ void check_scene(const at::Tensor& scene, int64_t n_spheres) {
   check_scene_shape(scene, n_spheres);
 }
 
+// Blobs whose headers passed, keyed by the tensor object (held weakly: a live entry cannot be a freed
+// tensor's address reused by a new one), its data pointer, size and version counter (bumped by every
+// in-place write): a blob is read back once per content version, not on every call, so repeated
+// renders of one scene stay asynchronous.
+struct CheckedBlob {
+  c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl> impl{
+      c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>::reclaim(
+          c10::UndefinedTensorImpl::singleton())};
+  const void* data = nullptr;
+  int64_t numel = -1, version = -1, n_spheres = -1;
+  bool matches(const at::Tensor& t, int64_t ns) const {
+    return !impl.expired() && impl._unsafe_get_target() == t.unsafeGetTensorImpl() && data == t.data_ptr() &&
+           numel == t.numel() && version == t._version() && n_spheres == ns;
+  }
+};
+constexpr int kCheckedBlobs = 32;
+std::mutex g_checked_mu;
+CheckedBlob g_checked[kCheckedBlobs];
+int g_checked_next = 0;
+
 // The header words of F blobs (rows of a [F, L] tensor, or one 1-D blob) against n_spheres: the
-// host-side form of the kernel's RTX_ST_BAD_SCENE test (one synchronous copy of 2 words per blob).
+// host-side form of the kernel's RTX_ST_BAD_SCENE test (one synchronous copy of 2 words per blob,
+// once per blob content: see CheckedBlob).
 void check_headers(const at::Tensor& blobs, int64_t n_spheres) {
+  {
+    std::lock_guard<std::mutex> lock(g_checked_mu);
+    for (const CheckedBlob& c : g_checked)
+      if (c.matches(blobs, n_spheres)) return;
+  }
   const at::Tensor head = (blobs.dim() == 1 ? blobs.narrow(0, 0, 2).unsqueeze(0) : blobs.narrow(1, 0, 2)).to(at::kCPU);
   const auto h = head.contiguous();
   const double* w = h.data_ptr<double>();
@@ -83,6 +111,14 @@ void check_headers(const at::Tensor& blobs, int64_t n_spheres) {
     TORCH_CHECK(w[2 * f + RTX_H_NSPH] == (double)n_spheres, "n_spheres=", n_spheres, " but scene blob ", f,
                 " holds ", w[2 * f + RTX_H_NSPH], " spheres");
   }
+  std::lock_guard<std::mutex> lock(g_checked_mu);
+  CheckedBlob& c = g_checked[g_checked_next];
+  g_checked_next = (g_checked_next + 1) % kCheckedBlobs;
+  c.impl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>(blobs.getIntrusivePtr());
+  c.data = blobs.data_ptr();
+  c.numel = blobs.numel();
+  c.version = blobs._version();
+  c.n_spheres = n_spheres;
 }
 
 // After a launch: read and clear the sticky status flags when the launch can set them (chains
@@ -96,6 +132,7 @@ void check_status_after(at::Tensor& ws, int64_t max_bounces) {
   TORCH_CHECK(!(st & RTX_ST_STACK_OVERFLOW), "maximum recursion depth exceeded (reflection chain > ",
               RTX_UNBOUNDED_LEVELS, " levels; HipRenderer raises RecursionError)");
   TORCH_CHECK(!(st & RTX_ST_BAD_SCENE), "the scene blob's header disagrees with n_spheres: nothing was rendered");
+  TORCH_CHECK(!(st & RTX_ST_UNRENDERED), "a render passed RTX_F_NO_GENERAL but deferred rays: pixels unwritten");
   TORCH_CHECK(false, "render status flags ", st, " (RTX_ST_LIST_OVERFLOW: deferred list full)");
 }
 

@@ -176,6 +176,7 @@ struct Params {
   int n_frames;
   int frame;  // set per block / per deferred ray (kernel side)
   uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null
+  int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred
 };
 
 // Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
@@ -205,8 +206,14 @@ __host__ __device__ constexpr int64_t records_cap(int64_t n, int pass) {
   return n < want ? n : want;
 }
 
-// append one entry to the launch's deferred list; returns its slot (or -1 when the list is full)
+// append one entry to the launch's deferred list; returns its slot (or -1 when the list is full).
+// Under RTX_F_NO_GENERAL no general kernel follows: the entry is dropped and RTX_ST_UNRENDERED raised
+// (the pixel stays unwritten, the list and its counter stay clean for the next call).
 __device__ __forceinline__ int64_t append_deferred(const Params& p, uint64_t entry) {
+  if (p.no_general) {
+    atomicOr((uint32_t*)p.ws + RTX_WS_STATUS, (uint32_t)RTX_ST_UNRENDERED);
+    return -1;
+  }
   const uint32_t slot = atomicAdd(p.dcount, 1u);
   if ((int64_t)slot < p.list_cap) {
     p.dlist[slot] = entry;
@@ -2497,6 +2504,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
   const bool capped = p.max_bounces >= 0 && p.max_bounces <= kCappedMax;
+  p.no_general = no_general && capped ? 1 : 0;
   p.n_workers = workers_for(n_all, p.max_bounces);
   p.stack_levels = stack_levels_for(p.max_bounces);
   {

@@ -40,6 +40,7 @@ OUT_U8_HWC = 2
 ST_STACK_OVERFLOW = 1
 ST_LIST_OVERFLOW = 2
 ST_BAD_SCENE = 4
+ST_UNRENDERED = 8  # RTX_F_NO_GENERAL render deferred rays: those pixels are unwritten
 
 F_NO_GENERAL = 1  # rtx_render_camera_ex flags
 

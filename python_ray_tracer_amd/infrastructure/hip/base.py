@@ -222,7 +222,7 @@ class HipRenderer(Renderer):
             raise ValueError(f"color_dtype must be float32 or float64, got {color_dtype}")
         self.max_bounces = None if max_bounces is None else int(max_bounces)
         self.color_dtype = color_dtype
-        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.device = _resolve_device(device)
         self._scene_cache: dict = {}
         # capped camera renders known to defer no ray (or probing): see _general_plan
         self._defers: dict = {}
@@ -572,6 +572,16 @@ class HipRenderer(Renderer):
     def reset_stats(self) -> None:
         if self.stats_buffer is not None:
             self.stats_buffer.zero_()
+
+
+def _resolve_device(device) -> torch.device:
+    """The renderer's device with an explicit index: None and an index-less "cuda" mean the
+    current device at construction (``_on_device`` switches to ``device.index``, which must not be
+    None). Anything but a ROCm device is refused: there is no CPU path."""
+    d = torch.device("cuda") if device is None else torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"HipRenderer renders on a ROCm device ('cuda[:N]'), got {d}")
+    return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
 
 
 def _as_vector(v) -> HipVector3D:

@@ -1,0 +1,311 @@
+"""The A/B patch set: named source rewrites of ``csrc/rtx_kernels.hip`` for ``tools/ab_build.py``.
+
+    python tools/ab_build.py OUT.so --patch NAME[,NAME...]
+
+Each patch is ``f(src) -> src``; it asserts its anchors, so a patch whose anchor left the source
+fails loudly instead of building the baseline under another name. Three kinds:
+
+* **variants** — the same output by other instructions; timed against the shipped build by
+  ``tools/ab.py`` (which checks the frames are equal);
+* **ablations** — timing only, wrong output (what a stage costs);
+* **instruments** — the shipped arithmetic plus measurement (``tile_trace``).
+
+Where each experiment's result lives:
+
+| patch | kind | result |
+|---|---|---|
+| ``inlgen`` | ablation | the general kernel carried behind a never-taken branch: C2 +68% (r2) |
+| ``nogen`` / ``tinygen`` | ablation | the tie launch removed / a trivial kernel in its place (r2_ab_variants) |
+| ``nolit`` / ``noshadow`` | ablation | no shadow walk in culled scenes / no shadow test (r2_ab_variants) |
+| ``pair_nobranch`` | variant | both roots of a sphere pair in every lane: +7..11% (r3f) |
+| ``tex_select`` | variant | hit_color's texture colour by selects: within noise (r3f) |
+| ``v_always`` | variant | V normalised for every hit: within noise (r3f) |
+| ``lv_together`` / ``self_triple`` / ``lv_triple`` | variant | ILP in shade(): r3p, not adopted |
+| ``tile_trace`` | instrument | per-tile start/end timestamps of k_render_fast (``tools/tile_trace.py``) |
+
+(The round-2/3 patches were written against the source of their session; their anchors are kept
+as they were, so they document the experiment and re-apply to that revision with ``--rev``.)
+"""
+
+from __future__ import annotations
+
+
+def _sub(src: str, old: str, new: str) -> str:
+    if old not in src:
+        raise SystemExit(f"ab_patches: anchor not found: {old[:100]!r}")
+    return src.replace(old, new)
+
+
+# ---------------------------------------------------------------------------------------------- ablations
+def inlgen(src: str) -> str:
+    """k_render_fast carries the general kernel's depth-first path behind a branch that is never
+    taken (mode 7): what its registers / scratch cost the fast path."""
+    a = "  fast_tile<B, LDS, DEEP, LVL, STATS>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);\n}"
+    src = _sub(src, a, a[:-1] + "  if (p.mode == 7) general_tail(p);\n}")
+    b = "template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false>"
+    src = _sub(src, b, "__device__ void general_tail(const Params& p);\n" + b)
+    c = "__global__ __launch_bounds__(64) void k_render_general(Params p0) {"
+    return _sub(src, c, """__device__ void general_tail(const Params& p) {
+  Stack S{p.stack, p.n_workers, (int64_t)blockIdx.x * kFastBlock + threadIdx.x};
+  double cr, cg, cb;
+  trace_general(p, S, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0, cr, cg, cb, -1, -1);
+  write_out(p, 0, cr, cg, cb);
+}
+
+""" + c)
+
+
+_GEN_LAUNCH = "  hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);"
+
+
+def nogen(src: str) -> str:
+    """No tie launch for capped renders (timing only: wrong when a frame has ties)."""
+    return _sub(src, _GEN_LAUNCH, "  if (!capped)" + _GEN_LAUNCH[1:])
+
+
+def tinygen(src: str) -> str:
+    """The tie launch replaced by a trivial kernel of the same grid that only reads the counters:
+    the cost of a second launch apart from k_render_general's own properties."""
+    src = _sub(src, _GEN_LAUNCH, """  if (capped) {
+    hipLaunchKernelGGL(k_noop_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);
+  } else {
+  """ + _GEN_LAUNCH + "\n  }")
+    b = "// ------------------------------------------------------------------------------------------\n// boundary helpers"
+    return _sub(src, b, """__global__ __launch_bounds__(64) void k_noop_general(Params p) {
+  uint32_t* hdr = (uint32_t*)p.ws;
+  if (hdr[RTX_WS_COUNT] != 0u && threadIdx.x == 0) hdr[RTX_WS_STATUS] |= 8u;
+}
+
+""" + b)
+
+
+def nolit(src: str) -> str:
+    """Culled scenes skip the shadow walk (timing only, wrong output)."""
+    return _sub(src, "  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);",
+                "  // ablation: no shadow walk for culled scenes (timing only)")
+
+
+def noshadow(src: str) -> str:
+    """No shadow test at all: lit = true (timing only, wrong output)."""
+    src = _sub(src, "  const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);",
+               "  const double tself = 1.0;  // ablation")
+    return _sub(src, "  const int nshadow = culled ? 0 : nsph - (hs < nsph);", "  const int nshadow = 0;  // ablation")
+
+
+# ---------------------------------------------------------------------------------------------- variants
+def pair_nobranch(src: str) -> str:
+    """The sphere-pair test computes both roots in every lane (no 'any lane may hit' branch)."""
+    old = """__device__ __forceinline__ void isect_pair(const SphTest& a, const SphTest& b, F&& f) {
+  if (!a.skip || !b.skip) {
+    bool v0, v1;
+    const double t0 = isect_sol(a, v0);
+    const double t1 = isect_sol(b, v1);
+    f(t0, v0, t1, v1);
+  }
+}"""
+    return _sub(src, old, """__device__ __forceinline__ void isect_pair(const SphTest& a, const SphTest& b, F&& f) {
+  bool v0, v1;
+  const double t0 = isect_sol(a, v0);
+  const double t1 = isect_sol(b, v1);
+  f(t0, v0, t1, v1);
+}""")
+
+
+def tex_select(src: str) -> str:
+    """hit_color's texture colour by selects instead of branches (IMG = false)."""
+    old = """  double tr, tg, tb;
+  const double tex = mh[RTX_M_TEX];
+  if (tex == RTX_TEX_CHECKER) {  // TextureChecker.get_color (:29-32): white * checker
+    tr = tg = tb = tk ? 1.0 : 0.0;
+  } else if (IMG && tex == RTX_TEX_IMAGE) {"""
+    return _sub(src, old, """  double tr, tg, tb;
+  const double tex = mh[RTX_M_TEX];
+  if (!IMG) {
+    const bool ck = tex == RTX_TEX_CHECKER;
+    const double c = tk ? 1.0 : 0.0;
+    tr = ck ? c : (double)mh[RTX_M_TR];
+    tg = ck ? c : (double)mh[RTX_M_TG];
+    tb = ck ? c : (double)mh[RTX_M_TB];
+  } else if (tex == RTX_TEX_CHECKER) {  // TextureChecker.get_color (:29-32): white * checker
+    tr = tg = tb = tk ? 1.0 : 0.0;
+  } else if (IMG && tex == RTX_TEX_IMAGE) {""")
+
+
+def v_always(src: str) -> str:
+    """The view vector is normalised for every hit (no weighted || need_irid branch)."""
+    return _sub(src, "  if (weighted || need_irid) {\n    double vx = sc[RTX_H_CAM + 0] - px",
+                "  {\n    double vx = sc[RTX_H_CAM + 0] - px")
+
+
+def lv_together(src: str) -> str:
+    """V (shader.py:76) normalised beside L (:75), before the shadow test: two square-root /
+    division chains in one basic block (bit-identical arithmetic; V computed for every hit)."""
+    src = _sub(src, """  double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
+  norm3(lx, ly, lz);  // :75
+""", """  double lx = sc[RTX_H_LIGHT + 0] - px, ly = sc[RTX_H_LIGHT + 1] - py, lz = sc[RTX_H_LIGHT + 2] - pz;
+  double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
+  {  // :75 and :76, the two chains interleaved (norm3's range ballot for L, V's core as before)
+    const double dl = dot3(lx, ly, lz, lx, ly, lz), dv = dot3(vx, vy, vz, vx, vy, vz);
+    double rl, rv;
+    if (__ballot(!(dl >= 0x1.0p-600 && dl <= 0x1.0p+600)) == 0) {
+      rl = div_core(1.0, sqrt_core(dl));
+      rv = inv_mag_shade_v(dv);
+    } else {
+      rl = inv_mag(dl);
+      rv = inv_mag_shade_v(dv);
+    }
+    lx = lx * rl; ly = ly * rl; lz = lz * rl;
+    vx = vx * rv; vy = vy * rv; vz = vz * rv;
+  }
+""")
+    return _sub(src, """  if (weighted || need_irid) {
+    double vx = sc[RTX_H_CAM + 0] - px, vy = sc[RTX_H_CAM + 1] - py, vz = sc[RTX_H_CAM + 2] - pz;
+    {  // :76 (towards the camera on every level); V only feeds the specular and the iridescence
+      const double rv = inv_mag_shade_v(dot3(vx, vy, vz, vx, vy, vz));
+      vx = vx * rv;
+      vy = vy * rv;
+      vz = vz * rv;
+    }
+    if (weighted)""", "  if (weighted || need_irid) {\n    if (weighted)")
+
+
+def self_triple(src: str) -> str:
+    """The shape's own shadow test (t_self, shader.py:126) evaluated with the first pair of the
+    other spheres' tests under one 'any lane may hit' branch (round-3 shade(), r3p)."""
+    old = """  const double qq = dot3(qx, qy, qz, qx, qy, qz);
+  const double tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
+  wk.test(1);
+  bool lit = true;
+  // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
+  // shadows. The linear loop handles it exactly; the culling tree skips missing spheres, so such
+  // a wave takes the linear loop.
+  const bool far_self = tself > FARAWAY;
+  // The shape's own test is t_self itself (same expression), and t_self < t_self never holds: when
+  // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
+  const int h0 = __builtin_amdgcn_readfirstlane(h);
+  const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
+  const bool culled = TREE && sc[RTX_H_NNODES] != 0.0 && __ballot(far_self) == 0;
+  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
+  const int nshadow = culled ? 0 : nsph - (hs < nsph);
+  int j = 0;
+"""
+    new = """  const double qq = dot3(qx, qy, qz, qx, qy, qz);
+  wk.test(1);
+  bool lit = true;
+  // The shape's own test is t_self itself (same expression), and t_self < t_self never holds: when
+  // every active lane hit the same sphere, the loops skip it (wave-uniform index remap below).
+  const int h0 = __builtin_amdgcn_readfirstlane(h);
+  const int hs = __ballot(h != h0) == 0 ? h0 : nsph;
+  const bool tree_scene = TREE && sc[RTX_H_NNODES] != 0.0;
+  const int nlin = nsph - (hs < nsph);
+  double tself;
+  bool far_self;
+  int j = 0;
+  bool first_pair_done = false;
+  if (!tree_scene && nlin >= 2) {
+    // t_self and the first pair of other spheres: three independent chains, one branch
+    const int j0 = __builtin_amdgcn_readfirstlane(0 + (0 >= hs));
+    const int j1 = __builtin_amdgcn_readfirstlane(1 + (1 >= hs));
+    const G* g0 = geo + j0 * RTX_GEOM_WORDS;
+    const G* g1 = geo + j1 * RTX_GEOM_WORDS;
+    wk.test(2);
+    const SphTest as = isect_disc(gh, qx, qy, qz, qq, lx, ly, lz, tame);
+    const SphTest a0 = isect_disc(g0, qx, qy, qz, qq, lx, ly, lz, tame);
+    const SphTest a1 = isect_disc(g1, qx, qy, qz, qq, lx, ly, lz, tame);
+    tself = FARAWAY;
+    bool sh = false;
+    if (!as.skip || !a0.skip || !a1.skip) {
+      bool vs, v0, v1;
+      const double ts = isect_sol(as, vs);
+      const double t0 = isect_sol(a0, v0);
+      const double t1 = isect_sol(a1, v1);
+      if (vs) tself = ts;
+      const bool fs = tself > FARAWAY;
+      sh = shadows(v0, t0, tself, fs) || shadows(v1, t1, tself, fs);
+    }
+    far_self = tself > FARAWAY;
+    if (sh) lit = false;
+    j = 2;
+    first_pair_done = true;
+  } else {
+    tself = isect_t(gh, qx, qy, qz, qq, lx, ly, lz, tame);
+    // t_self beyond FARAWAY (a hit past the reference's sentinel distance): every missing sphere
+    // shadows. The linear loop handles it exactly; the culling tree skips missing spheres, so such
+    // a wave takes the linear loop.
+    far_self = tself > FARAWAY;
+  }
+  const bool culled = tree_scene && __ballot(far_self) == 0;
+  if (culled) lit = lit_bvh(sc, qx, qy, qz, qq, lx, ly, lz, tself, hs, tame, wk);
+  const int nshadow = culled ? 0 : nlin;
+  if (first_pair_done && !lit) j = nshadow;  // shadowed by the first pair: the loops end here
+"""
+    src = _sub(src, old, new)
+    old = """  if (lit && j < nshadow) {
+    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;"""
+    new = """  if (lit && j < nshadow) {  // (the loop above breaks with j < nshadow only when lit is false)
+    const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;"""
+    return _sub(src, old, new)
+
+
+def lv_triple(src: str) -> str:
+    return self_triple(lv_together(src))
+
+
+# ---------------------------------------------------------------------------------------------- instruments
+TRACE_WORDS = 4  # per record: t_start, t_end (s_memrealtime, 100 MHz), tile id, hw id | xcc id << 32
+
+
+def tile_trace(src: str) -> str:
+    """Per-tile timestamps of k_render_fast: every wave records (start, end, tile, hardware id) of
+    each tile it renders into a device buffer registered with ``rtx_trace_set(buf)`` (word 0: the
+    record counter, word 1: capacity, records from word 8). The persistent loop times each fetched
+    tile; the one-tile-per-block path times the wave from kernel entry (scene staging included).
+    s_memrealtime is the 100 MHz constant clock; the arithmetic of the render is unchanged."""
+    src = _sub(src, "  uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null\n};",
+               "  uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null\n"
+               "  unsigned long long* trace;  // tile_trace instrument\n};")
+    rec = """
+__device__ __forceinline__ void trace_rec(const Params& p, unsigned long long t0, unsigned long long id) {
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (p.trace && (threadIdx.x & 63) == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
+    const unsigned long long k = atomicAdd(p.trace, 1ull);
+    if (k < p.trace[1]) {
+      unsigned long long* r = p.trace + 8 + 4 * k;
+      r[0] = t0; r[1] = t1; r[2] = id; r[3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    }
+  }
+}
+"""
+    anchor = "// TP: 0 = no culling tree and no persistent launch"
+    src = _sub(src, anchor, rec + "\n" + anchor)
+    src = _sub(src, "  const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)\n",
+               "  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();\n"
+               "  const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)\n")
+    old = ("      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, "
+           "false, lds_tab, true);\n")
+    src = _sub(src, old, "      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();\n" + old +
+               "      trace_rec(p, t0, (unsigned long long)t | ((unsigned long long)pw << 32));\n")
+    old = "  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);\n}"
+    src = _sub(src, old, old[:-1] + "  trace_rec(p, t_entry, ((unsigned long long)(blockIdx.y * gridDim.x + blockIdx.x) * "
+               "kFastWaves + (threadIdx.x >> 6)) | (1ull << 63));\n}")
+    src = _sub(src, "int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {\n",
+               "unsigned long long* g_trace = nullptr;\n"
+               "int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {\n"
+               "  p.trace = g_trace;\n")
+    return _sub(src, "const char* rtx_last_error(void) { return g_err; }\n",
+                "const char* rtx_last_error(void) { return g_err; }\n\n"
+                "int rtx_trace_set(void* buf) {\n  g_trace = (unsigned long long*)buf;\n  return RTX_OK;\n}\n")
+
+
+PATCHES = {f.__name__: f for f in (inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
+                                   lv_together, self_triple, lv_triple, tile_trace)}
+
+
+def apply(src: str, names: str) -> str:
+    for name in [n for n in names.split(",") if n]:
+        if name not in PATCHES:
+            raise SystemExit(f"unknown patch {name!r}; known: {', '.join(PATCHES)}")
+        src = PATCHES[name](src)
+    return src
