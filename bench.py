@@ -356,7 +356,8 @@ def tiles_stepper(r, scene, world, row_block, out):
         return step1, (lambda: None)
     from python_ray_tracer_amd.distributed import TileGather
 
-    tg = TileGather(r, int(scene.camera.width), int(scene.camera.height), row_block=row_block, out=out, slots=2)
+    tg = TileGather(r, int(scene.camera.width), int(scene.camera.height), row_block=row_block, out=out, slots=2,
+                    persistent_frames=True)
     state = {"k": 0, "open": None}
 
     def step():

@@ -212,7 +212,8 @@ enum {
   RTX_OK = 0,
   RTX_E_ARG = -1,     /* bad argument (null pointer, size, kind)  */
   RTX_E_LAUNCH = -2,  /* HIP launch / runtime error               */
-  RTX_E_WORKSPACE = -3 /* workspace too small                     */
+  RTX_E_WORKSPACE = -3, /* workspace too small                    */
+  RTX_E_COMM = -4      /* RCCL missing, or an RCCL call failed      */
 };
 
 /* Library version (RTX_ABI_VERSION) and the layout constants above, for the host to verify:
@@ -305,6 +306,51 @@ int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, 
  * (the largest). */
 int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts, int width, int height,
                       int row_block, int kind, void* out, void* stream);
+
+/* ---- the row-tiled multi-GPU frame, one call per frame and rank (csrc/rtx_tiles.hip) ----
+ * The north star's "framebuffer row-tiles across the GPUs of one node with an RCCL gather over
+ * xGMI": the reference renders one frame in one process (render_image_pipeline,
+ * application.py:43-52); python_ray_tracer_amd.distributed.TileGather drives these entry points.
+ * Every rank renders its interleaved row tile (as rtx_render_camera_ex with row_block, n_parts =
+ * world, part = rank); the root receives every peer's tile with one ncclRecv per peer inside one
+ * RCCL group (each peer's link carries its own bytes at once; a ring would be bound by one link)
+ * and un-permutes the rows on the device (rtx_assemble_rows). RCCL is the process's own librccl,
+ * resolved at run time (rtx_rccl_load): the library has no link-time RCCL dependency. */
+#define RTX_TILES_MAX_SLOTS 4
+/* dlopen the RCCL library at `path` (NULL: "librccl.so"), reusing it if the process already loaded
+ * it (torch's), and resolve the calls used here. Idempotent. */
+int rtx_rccl_load(const char* path);
+/* ncclGetUniqueId into id_out (128 bytes): the root calls it, the host broadcasts the bytes. */
+int rtx_comm_unique_id(void* id_out);
+/* ncclCommInitRank over `world` ranks (collective: every rank calls it with the same id); the
+ * communicator is bound to the current device. */
+int rtx_comm_init(const void* id, int world, int rank, void** comm_out);
+int rtx_comm_destroy(void* comm);
+/* rtx_tiles_create flags. RTX_TILES_LOOPBACK: a one-rank plan whose tile still travels through
+ * RCCL (sent to and received from itself, then assembled): the gather path on a single GPU. */
+#define RTX_TILES_LOOPBACK 1u
+/* A plan for frames of width x height in row blocks of row_block, out_kind RTX_OUT_*, `slots`
+ * frames in flight (<= RTX_TILES_MAX_SLOTS). Per slot s, caller-owned device buffers kept for the
+ * plan's life: a peer's send[s] (part_bytes) and the root's recv[s] (world * part_bytes: part p at
+ * p * part_bytes). part_bytes holds part 0's tile (the largest), a multiple of 16. world == 1 needs
+ * neither buffers nor a communicator (comm NULL): the single part is the frame (unless
+ * RTX_TILES_LOOPBACK: then send and recv as a root and peer would). Creates the plan's own
+ * collective stream on the current device. */
+int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int height, int row_block, int out_kind,
+                     int slots, void* const* send, void* const* recv, int64_t part_bytes, unsigned flags,
+                     void** plan_out);
+/* Frame of slot `slot`: on `stream`, wait until the slot's previous frame has left its buffers, then
+ * render this rank's tile (scene, n_spheres, max_bounces, workspace, flags, deferred_out as
+ * rtx_render_camera_ex); then, on the plan's stream after the render, the RCCL gather to the root
+ * and (root) the assembly into `frame` (the root's whole frame, in a whole-frame render's layout;
+ * ignored on peers). Asynchronous; never synchronises. */
+int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, int max_bounces, void* workspace,
+                     size_t workspace_bytes, unsigned flags, uint32_t* deferred_out, void* frame, void* stream);
+/* Make `stream` wait until slot `slot`'s frame is complete (the root's frame is then valid in
+ * stream order). */
+int rtx_tiles_finish(void* plan, int slot, void* stream);
+/* Waits for the plan's stream, then frees its stream and events (not the caller's buffers). */
+int rtx_tiles_destroy(void* plan);
 
 /* Test hook: out[0:n] = the library's fast-path sqrt(a), out[n:2n] = the compiler's full sqrt(a),
  * out[2n:3n] = fast-path a/b, out[3n:4n] = full a/b, out[4n:5n] = the renormalisation factor of an

@@ -12,6 +12,7 @@ PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 SRC = PKG / "csrc" / "rtx_kernels.hip"
 SMALL_SRC = PKG / "csrc" / "rtx_small.hip"  # includes SRC's device code
+TILES_SRC = PKG / "csrc" / "rtx_tiles.hip"  # host code: the row-tiled multi-GPU frame (RCCL at run time)
 HDR = REPO / "include" / "rtx_hip.h"
 LIB = PKG / "librtx_hip.so"
 OPS_SRC = PKG / "csrc" / "rt_ops.cpp"
@@ -40,7 +41,30 @@ def needs_build() -> bool:
     if not LIB.exists():
         return True
     t = LIB.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in (SRC, SMALL_SRC, HDR, Path(__file__)))
+    return any(p.stat().st_mtime > t for p in (SRC, SMALL_SRC, TILES_SRC, HDR, Path(__file__)))
+
+
+OBJ_CACHE = PKG / ".objcache"  # compiled units by content hash (a one-unit change rebuilds one unit)
+
+
+def _unit_key(src: Path, flags) -> str:
+    """Hash of a unit's text, the text of every file it #includes (recursively, quoted includes) and
+    its compile command's flags."""
+    import hashlib
+    import re
+
+    h = hashlib.sha256()
+    seen, todo = set(), [src.resolve()]
+    while todo:
+        f = todo.pop()
+        if f in seen or not f.exists():
+            continue
+        seen.add(f)
+        text = f.read_bytes()
+        h.update(str(f.name).encode() + b"\0" + text)
+        todo += [(f.parent / m.decode()).resolve() for m in re.findall(rb'#include\s+"([^"]+)"', text)]
+    h.update(repr([hipcc(), *flags]).encode())
+    return h.hexdigest()[:32]
 
 
 def compile_units(out: Path, main_src: Path, small_src: Path | None, extra_flags=(), verbose: bool = False,
@@ -51,22 +75,36 @@ def compile_units(out: Path, main_src: Path, small_src: Path | None, extra_flags
 
     sf = list(SMALL_FLAGS if small_flags is None else small_flags)
     units = [(main_src, [])] + ([(small_src, sf)] if small_src is not None else [])
+    if small_src is not None and TILES_SRC.exists():  # (single-unit revisions of the A/B tool build alone)
+        units.append((TILES_SRC, []))
     objs, procs = [], []
     # objects in a directory of this call's own: concurrent builds (several ranks importing on a
     # fresh checkout) cannot overwrite or delete each other's objects before the link
     objdir = Path(tempfile.mkdtemp(prefix=f".{out.stem}.", dir=str(out.parent)))
     try:
+        OBJ_CACHE.mkdir(exist_ok=True)
+        fresh = []
         for src, flags in units:
+            allf = [*HIPCC_FLAGS, *flags, *extra_flags]
+            cached = OBJ_CACHE / f"{src.stem}.{_unit_key(src, allf)}.o"
+            if cached.exists():
+                objs.append(cached)
+                continue
             obj = objdir / f"{src.stem}.o"
-            cmd = [hipcc(), *HIPCC_FLAGS, *flags, *extra_flags, "-c", "-o", str(obj), str(src)]
+            cmd = [hipcc(), *allf, "-c", "-o", str(obj), str(src)]
             if verbose:
                 print(" ".join(cmd))
             objs.append(obj)
+            fresh.append((obj, cached))
             procs.append((subprocess.Popen(cmd, cwd=str(REPO)), cmd))
         for proc, cmd in procs:
             if proc.wait() != 0:
                 raise subprocess.CalledProcessError(proc.returncode, cmd)
-        cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *map(str, objs)]
+        for obj, cached in fresh:  # keep the new objects (renamed whole: concurrent builds stay safe)
+            tmp = cached.with_suffix(f".o.tmp{os.getpid()}")
+            shutil.copyfile(obj, tmp)
+            os.replace(tmp, cached)
+        cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *map(str, objs), "-ldl"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True, cwd=str(REPO))

@@ -2828,4 +2828,10 @@ int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts,
 
 }  // extern "C"
 
+// the error message of the other host units (csrc/rtx_tiles.hip), read through rtx_last_error
+__attribute__((visibility("hidden"))) int rtx_set_error(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
 #endif  // RTX_DEVICE_CODE_ONLY

@@ -1,0 +1,282 @@
+// rtx_tiles.hip — the row-tiled multi-GPU frame driven natively (the north star's
+// "framebuffer row-tiles across the GPUs of one node with an RCCL gather over xGMI"). The reference
+// renders a frame in one process (render_image_pipeline, application.py:43-52); here every rank
+// renders its interleaved row tile (rtx_render_camera_ex), the root receives the peers' tiles over
+// RCCL point-to-point (one ncclRecv per peer inside one group: each peer's bytes arrive over its own
+// xGMI link at once, where a ring would be bound by one link) and un-permutes the rows on the device
+// (rtx_assemble_rows). One call per frame and rank submits all of it — no Python between the render,
+// the collective and the assembly (distributed.TileGather drives it).
+//
+// Streams: the render runs on the caller's stream; the collective and the assembly on the plan's
+// own stream, after an event, so frame k's gather runs while frame k+1 renders (two slots). A slot's
+// buffers are reused only after its previous frame's gather and assembly have completed (event).
+//
+// RCCL is the process's own librccl (the one torch loaded: the same library instance must create
+// and drive a communicator), resolved at run time with dlopen/dlsym; <rccl/rccl.h> supplies types
+// only. The library has no link-time RCCL dependency, so the single-GPU entry points load without it.
+// Host code only: no kernels in this unit.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/rtx_hip.h"
+
+// rtx_kernels.hip: the library's thread-local error message
+__attribute__((visibility("hidden"))) int rtx_set_error(int code, const char* msg);
+
+namespace {
+
+struct Rccl {
+  void* lib = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+Rccl g_rccl;
+std::mutex g_rccl_mu;
+
+int err(int code, const char* fmt, const char* a = "", long long b = 0) {
+  char m[512];
+  snprintf(m, sizeof(m), fmt, a, b);
+  return rtx_set_error(code, m);
+}
+
+int nccl_err(const char* what, ncclResult_t r) {
+  char m[512];
+  snprintf(m, sizeof(m), "%s: %s", what, g_rccl.error_string ? g_rccl.error_string(r) : "RCCL error");
+  return rtx_set_error(RTX_E_COMM, m);
+}
+
+bool rccl_ready() { return g_rccl.send != nullptr; }
+
+template <typename F>
+bool sym(F& f, const char* name) {
+  f = reinterpret_cast<F>(dlsym(g_rccl.lib, name));
+  return f != nullptr;
+}
+
+// A row-tiled frame plan: one rank's view of the frame (its tile, the communicator, the slots'
+// buffers and events). Buffers are caller-owned device memory registered once.
+struct Tiles {
+  ncclComm_t comm;
+  int world, rank, root;
+  int width, height, row_block, out_kind;
+  int slots;
+  int64_t part_bytes;
+  int local_rows;
+  int device;
+  bool loop;  // RTX_TILES_LOOPBACK: a one-rank plan whose tile still goes through RCCL (send to itself)
+  hipStream_t cs;  // collective + assembly stream
+  void* send[RTX_TILES_MAX_SLOTS];
+  void* recv[RTX_TILES_MAX_SLOTS];
+  hipEvent_t rendered[RTX_TILES_MAX_SLOTS];
+  hipEvent_t done[RTX_TILES_MAX_SLOTS];
+  bool used[RTX_TILES_MAX_SLOTS];
+};
+
+int local_rows(int height, int row_block, int n_parts, int p) {  // tiling.n_local_rows
+  const int cycle = row_block * n_parts;
+  const int q = height / cycle, rem = height % cycle - p * row_block;
+  return q * row_block + (rem < 0 ? 0 : rem > row_block ? row_block : rem);
+}
+
+int64_t bytes_per_pixel(int kind) { return kind == RTX_OUT_F32_SOA ? 12 : kind == RTX_OUT_F64_SOA ? 24 : 3; }
+
+}  // namespace
+
+extern "C" {
+
+int rtx_rccl_load(const char* path) {
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  if (rccl_ready()) return RTX_OK;
+  // the library torch (or the caller) already loaded, if any: RTLD_NOLOAD returns its handle
+  void* h = dlopen(path && *path ? path : "librccl.so", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen(path && *path ? path : "librccl.so", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    const char* why = dlerror();
+    return err(RTX_E_COMM, "cannot load RCCL (%s)", why ? why : "dlopen failed");
+  }
+  g_rccl = Rccl{};
+  g_rccl.lib = h;
+  bool ok = sym(g_rccl.get_unique_id, "ncclGetUniqueId") && sym(g_rccl.comm_init_rank, "ncclCommInitRank") &&
+            sym(g_rccl.comm_destroy, "ncclCommDestroy") && sym(g_rccl.recv, "ncclRecv") &&
+            sym(g_rccl.group_start, "ncclGroupStart") && sym(g_rccl.group_end, "ncclGroupEnd") &&
+            sym(g_rccl.error_string, "ncclGetErrorString") && sym(g_rccl.send, "ncclSend");
+  if (!ok) {
+    g_rccl = Rccl{};
+    return err(RTX_E_COMM, "RCCL library lacks a required symbol%s", "");
+  }
+  return RTX_OK;
+}
+
+int rtx_comm_unique_id(void* id_out) {
+  if (!id_out) return err(RTX_E_ARG, "null pointer argument%s", "");
+  if (!rccl_ready()) return err(RTX_E_COMM, "RCCL not loaded (rtx_rccl_load)%s", "");
+  ncclUniqueId id;
+  if (ncclResult_t r = g_rccl.get_unique_id(&id)) return nccl_err("ncclGetUniqueId", r);
+  memcpy(id_out, &id, sizeof(id));
+  return RTX_OK;
+}
+
+int rtx_comm_init(const void* id, int world, int rank, void** comm_out) {
+  if (!id || !comm_out) return err(RTX_E_ARG, "null pointer argument%s", "");
+  if (world < 1 || rank < 0 || rank >= world) return err(RTX_E_ARG, "bad world/rank%s (%lld)", "", world);
+  if (!rccl_ready()) return err(RTX_E_COMM, "RCCL not loaded (rtx_rccl_load)%s", "");
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  if (ncclResult_t r = g_rccl.comm_init_rank(&c, world, uid, rank)) return nccl_err("ncclCommInitRank", r);
+  *comm_out = c;
+  return RTX_OK;
+}
+
+int rtx_comm_destroy(void* comm) {
+  if (!comm) return RTX_OK;
+  if (!rccl_ready()) return err(RTX_E_COMM, "RCCL not loaded%s", "");
+  if (ncclResult_t r = g_rccl.comm_destroy((ncclComm_t)comm)) return nccl_err("ncclCommDestroy", r);
+  return RTX_OK;
+}
+
+int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int height, int row_block, int out_kind,
+                     int slots, void* const* send, void* const* recv, int64_t part_bytes, unsigned flags,
+                     void** plan_out) {
+  if (!plan_out) return err(RTX_E_ARG, "null plan pointer%s", "");
+  *plan_out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world || root < 0 || root >= world)
+    return err(RTX_E_ARG, "bad world/rank/root%s (%lld)", "", world);
+  if (width <= 0 || height <= 0 || row_block <= 0) return err(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  if (out_kind < 0 || out_kind > 2) return err(RTX_E_ARG, "bad out_kind%s %lld", "", out_kind);
+  if (slots < 1 || slots > RTX_TILES_MAX_SLOTS) return err(RTX_E_ARG, "bad slot count%s (%lld)", "", slots);
+  if (flags & ~(unsigned)RTX_TILES_LOOPBACK) return err(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
+  const bool loop = world == 1 && (flags & RTX_TILES_LOOPBACK);
+  if ((world > 1 || loop) && (!comm || !rccl_ready()))
+    return err(RTX_E_COMM, "world > 1 (or a loopback plan) needs an RCCL communicator%s", "");
+  const int rows0 = local_rows(height, row_block, world, 0);  // part 0 has the most rows
+  if (part_bytes < rows0 * (int64_t)width * bytes_per_pixel(out_kind) || part_bytes % 16 != 0)
+    return err(RTX_E_ARG, "part_bytes must hold part 0's tile and be a multiple of 16%s (%lld)", "", part_bytes);
+  for (int s = 0; s < slots; ++s) {
+    if (rank == root && (world > 1 || loop) && (!recv || !recv[s]))
+      return err(RTX_E_ARG, "the root needs a receive buffer per slot%s", "");
+    if ((rank != root || loop) && (!send || !send[s]))
+      return err(RTX_E_ARG, "a peer (or a loopback plan) needs a send buffer per slot%s", "");
+  }
+  Tiles* t = new Tiles{};
+  t->comm = (ncclComm_t)comm;
+  t->world = world;
+  t->rank = rank;
+  t->root = root;
+  t->width = width;
+  t->height = height;
+  t->row_block = row_block;
+  t->out_kind = out_kind;
+  t->slots = slots;
+  t->part_bytes = part_bytes;
+  t->local_rows = local_rows(height, row_block, world, rank);
+  t->loop = loop;
+  (void)hipGetDevice(&t->device);
+  hipError_t e = hipStreamCreateWithFlags(&t->cs, hipStreamNonBlocking);
+  for (int s = 0; s < slots && e == hipSuccess; ++s) {
+    t->send[s] = send ? send[s] : nullptr;
+    t->recv[s] = recv ? recv[s] : nullptr;
+    e = hipEventCreateWithFlags(&t->rendered[s], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->done[s], hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    rtx_tiles_destroy(t);
+    return err(RTX_E_LAUNCH, "rtx_tiles_create: %s", hipGetErrorString(e));
+  }
+  *plan_out = t;
+  return RTX_OK;
+}
+
+int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, int max_bounces, void* workspace,
+                     size_t workspace_bytes, unsigned flags, uint32_t* deferred_out, void* frame, void* stream) {
+  Tiles* t = (Tiles*)plan;
+  if (!t) return err(RTX_E_ARG, "null plan%s", "");
+  if (slot < 0 || slot >= t->slots) return err(RTX_E_ARG, "bad slot%s (%lld)", "", slot);
+  hipStream_t s = (hipStream_t)stream;
+  const bool root = t->rank == t->root;
+  if (root && !frame) return err(RTX_E_ARG, "the root needs a frame buffer%s", "");
+  // the slot's buffers are free once its previous frame's gather and assembly have run
+  if (t->used[slot]) {
+    if (hipError_t e = hipStreamWaitEvent(s, t->done[slot], 0))
+      return err(RTX_E_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  t->used[slot] = true;
+  // a single part IS the frame (local rows = global rows): render straight into it
+  void* dst = t->loop        ? t->send[slot]
+              : t->world == 1 ? frame
+              : root          ? (uint8_t*)t->recv[slot] + (int64_t)t->root * t->part_bytes
+                              : t->send[slot];
+  if (int rc = rtx_render_camera_ex(scene, n_spheres, t->width, t->height, t->row_block, t->world, t->rank,
+                                    t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes, nullptr,
+                                    stream, flags, deferred_out))
+    return rc;
+  if (t->world == 1 && !t->loop) {
+    if (hipError_t e = hipEventRecord(t->done[slot], s)) return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
+    return RTX_OK;
+  }
+  hipError_t e = hipEventRecord(t->rendered[slot], s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(t->cs, t->rendered[slot], 0);
+  if (e != hipSuccess) return err(RTX_E_LAUNCH, "event: %s", hipGetErrorString(e));
+  if (ncclResult_t r = g_rccl.group_start()) return nccl_err("ncclGroupStart", r);
+  ncclResult_t r = ncclSuccess;
+  if (t->loop) {
+    r = g_rccl.send(t->send[slot], (size_t)t->part_bytes, ncclUint8, 0, t->comm, t->cs);
+    if (r == ncclSuccess) r = g_rccl.recv(t->recv[slot], (size_t)t->part_bytes, ncclUint8, 0, t->comm, t->cs);
+  } else if (root) {
+    for (int p = 0; p < t->world && r == ncclSuccess; ++p) {
+      if (p == t->root) continue;
+      r = g_rccl.recv((uint8_t*)t->recv[slot] + (int64_t)p * t->part_bytes, (size_t)t->part_bytes, ncclUint8, p, t->comm,
+                      t->cs);
+    }
+  } else {
+    r = g_rccl.send(t->send[slot], (size_t)t->part_bytes, ncclUint8, t->root, t->comm, t->cs);
+  }
+  const ncclResult_t r2 = g_rccl.group_end();
+  if (r != ncclSuccess) return nccl_err(root ? "ncclRecv" : "ncclSend", r);
+  if (r2 != ncclSuccess) return nccl_err("ncclGroupEnd", r2);
+  if (root) {
+    if (int rc = rtx_assemble_rows(t->recv[slot], t->part_bytes, t->world, t->width, t->height, t->row_block,
+                                   t->out_kind, frame, t->cs))
+      return rc;
+  }
+  if ((e = hipEventRecord(t->done[slot], t->cs))) return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
+  return RTX_OK;
+}
+
+int rtx_tiles_finish(void* plan, int slot, void* stream) {
+  Tiles* t = (Tiles*)plan;
+  if (!t) return err(RTX_E_ARG, "null plan%s", "");
+  if (slot < 0 || slot >= t->slots) return err(RTX_E_ARG, "bad slot%s (%lld)", "", slot);
+  if (!t->used[slot]) return RTX_OK;
+  if (hipError_t e = hipStreamWaitEvent((hipStream_t)stream, t->done[slot], 0))
+    return err(RTX_E_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  return RTX_OK;
+}
+
+int rtx_tiles_destroy(void* plan) {
+  Tiles* t = (Tiles*)plan;
+  if (!t) return RTX_OK;
+  // the plan's stream may still run a gather: let it finish before its events go
+  if (t->cs) (void)hipStreamSynchronize(t->cs);
+  for (int s = 0; s < t->slots; ++s) {
+    if (t->rendered[s]) (void)hipEventDestroy(t->rendered[s]);
+    if (t->done[s]) (void)hipEventDestroy(t->done[s]);
+  }
+  if (t->cs) (void)hipStreamDestroy(t->cs);
+  delete t;
+  return RTX_OK;
+}
+
+}  // extern "C"

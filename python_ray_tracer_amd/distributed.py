@@ -15,6 +15,11 @@ stream, after the render), ``finish(slot)`` makes the current stream wait for it
 With two slots the gather of frame k runs while frame k+1 renders (``bench.py --mode tiles``).
 Under gloo (CPU tests, ranks sharing one GPU) tiles travel through host memory and every call is
 synchronous.
+
+Under RCCL with ``HipRenderer`` (``native``, the default there) a frame is ONE native call per rank
+(``rtx_tiles_submit``, csrc/rtx_tiles.hip): the render, the peers' RCCL sends / the root's receives
+(the library's own communicator over the same librccl torch loaded) and the root's assembly are
+enqueued without Python between them, on the caller's stream and the plan's collective stream.
 """
 
 from __future__ import annotations
@@ -27,9 +32,51 @@ import torch
 from python_ray_tracer_amd import tiling
 
 
+# RCCL communicators of the native path, one per (process group, rank, device): creating one costs
+# a rendezvous, so TileGathers of the same group share it for the life of the process
+_COMMS: dict = {}
+
+
+def rccl_comm(group, root: int, device):
+    """The library's RCCL communicator over ``group`` (rtx_comm_init): the root's ncclUniqueId is
+    broadcast over the group itself. Collective: every rank of the group calls it."""
+    import ctypes
+
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    pg = group if group is not None else dist.group.WORLD
+    world, rank = dist.get_world_size(pg), dist.get_rank(pg)
+    key = (getattr(pg, "group_name", id(pg)), world, rank, torch.device(device).index)
+    comm = _COMMS.get(key)
+    if comm is not None:
+        return comm
+    lib = L.load()
+    L.rccl_load()
+    uid = (ctypes.c_char * L.UNIQUE_ID_BYTES)()
+    if rank == root:
+        L.check(lib.rtx_comm_unique_id(uid), "rtx_comm_unique_id")
+    obj = [bytes(uid) if rank == root else None]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(pg, root), group=pg, device=torch.device(device))
+    uid = (ctypes.c_char * L.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+    c = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        L.check(lib.rtx_comm_init(uid, world, rank, ctypes.byref(c)), "rtx_comm_init")
+    _COMMS[key] = c.value
+    return c.value
+
+
 class TileGather:
     def __init__(self, renderer, width: int, height: int, *, group=None, row_block: int = 8, dst: int = 0,
-                 out: str | None = None, slots: int = 2) -> None:
+                 out: str | None = None, slots: int = 2, native: bool | None = None,
+                 persistent_frames: bool = False, loopback: bool = False) -> None:
+        """``native``: drive each frame through rtx_tiles_submit (default: under RCCL with a
+        renderer that has ``submit_tiles``); False keeps torch.distributed.gather. ``persistent_frames``
+        (native root): assemble every frame of a slot into one buffer kept by the slot, so a frame
+        returned by finish(slot) is overwritten by that slot's next frame (the bench); otherwise each
+        frame gets a new tensor. ``loopback`` (native, one rank): the tile still travels through RCCL
+        (sent to and received from the rank itself), the gather path on one GPU (tests)."""
         import torch.distributed as dist
 
         self._dist = dist
@@ -48,6 +95,13 @@ class TileGather:
         self.n = int(np.prod(self.shape))
         plen = tiling.part_len(self.H, self.W, self.rb, self.world, torch.empty((), dtype=dtype).element_size(),
                                self.out)
+        self._pending: dict = {}
+        self.plan = None
+        if native is None:
+            native = not self.gloo and hasattr(renderer, "submit_tiles")
+        if native:
+            self._init_native(dtype, plen, slots, persistent_frames, loopback and self.world == 1)
+            return
         # zero-filled once: the padding beyond a short part's tile is sent but never read
         self.send = [torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]
         coll = torch.device("cpu") if self.gloo else self.device
@@ -56,12 +110,58 @@ class TileGather:
         # the gather's per-rank views of each receive buffer, built once (not per frame)
         self._recv_lists = [list(b.unbind(0)) for b in self.recv] if self.recv is not None else None
         self._views = [b[:self.n].view(self.shape) for b in self.send]
-        self._pending: dict = {}
+
+    def _init_native(self, dtype, plen, slots, persistent_frames, loop) -> None:
+        import ctypes
+
+        from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+        if not 1 <= slots <= L.TILES_MAX_SLOTS:
+            raise ValueError(f"slots must be 1..{L.TILES_MAX_SLOTS}")
+        self._L = L
+        self._lib = L.load()
+        root = self.rank == self.dst
+        self.send = ([torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]
+                     if not root or loop else [])
+        self.recv = ([torch.zeros((self.world, plen), dtype=dtype, device=self.device) for _ in range(slots)]
+                     if root and (self.world > 1 or loop) else None)
+        self.frame_shape = (self.H, self.W, 3) if self.out == "u8" else (3, self.H * self.W)
+        self._dtype = dtype
+        self.frames = ([torch.empty(self.frame_shape, dtype=dtype, device=self.device) for _ in range(slots)]
+                       if root and persistent_frames else None)
+        comm = rccl_comm(self.group, self.dst, self.device) if self.world > 1 or loop else None
+        ptrs = ctypes.c_void_p * slots
+        send = ptrs(*[b.data_ptr() for b in self.send]) if self.send else None
+        recv = ptrs(*[b.data_ptr() for b in self.recv]) if self.recv else None
+        kind = L.OUT_U8_HWC if self.out == "u8" else (L.OUT_F64_SOA if dtype == torch.float64 else L.OUT_F32_SOA)
+        plan = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            L.check(self._lib.rtx_tiles_create(comm, self.world, self.rank, self.dst, self.W, self.H, self.rb, kind,
+                                               slots, send, recv, plen * torch.empty((), dtype=dtype).element_size(),
+                                               L.TILES_LOOPBACK if loop else 0, ctypes.byref(plan)),
+                    "rtx_tiles_create")
+        self.plan = plan.value
+
+    def __del__(self):
+        plan, self.plan = getattr(self, "plan", None), None
+        if plan is not None:
+            try:
+                self._lib.rtx_tiles_destroy(plan)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
 
     def submit(self, scene, slot: int = 0) -> None:
         """Render this rank's tile of ``scene`` into slot ``slot`` and start its gather."""
         if slot in self._pending:
             raise RuntimeError(f"slot {slot} still has a frame in flight: finish() it first")
+        if self.plan is not None:
+            frame = None
+            if self.rank == self.dst:
+                frame = (self.frames[slot] if self.frames is not None
+                         else torch.empty(self.frame_shape, dtype=self._dtype, device=self.device))
+            self.r.submit_tiles(self.plan, slot, scene, self.rb, self.world, self.rank, frame)
+            self._pending[slot] = (None, frame)
+            return
         buf = self.send[slot]
         view = self._views[slot]
         if self._into:
@@ -76,7 +176,13 @@ class TileGather:
     def finish(self, slot: int = 0):
         """Wait for slot ``slot``'s gather (a stream wait under nccl) and, on the root, assemble the
         frame: [3, H*W] colour or [H, W, 3] uint8. Other ranks return None."""
-        work, _ = self._pending.pop(slot)
+        work, frame = self._pending.pop(slot)
+        if self.plan is not None:
+            with torch.cuda.device(self.device):
+                self._L.check(self._lib.rtx_tiles_finish(self.plan, slot,
+                                                         self._L.stream_handle(torch.cuda.current_stream(self.device))),
+                              "rtx_tiles_finish")
+            return frame
         work.wait()
         if self.rank != self.dst:
             return None

@@ -82,7 +82,19 @@ EXPORTS = (
     "rtx_selftest_math",
     "rtx_assemble_rows",
     "rtx_shade_hits",
+    "rtx_rccl_load",
+    "rtx_comm_unique_id",
+    "rtx_comm_init",
+    "rtx_comm_destroy",
+    "rtx_tiles_create",
+    "rtx_tiles_submit",
+    "rtx_tiles_finish",
+    "rtx_tiles_destroy",
 )
+
+TILES_MAX_SLOTS = 4
+TILES_LOOPBACK = 1  # rtx_tiles_create flags
+UNIQUE_ID_BYTES = 128  # ncclUniqueId
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -111,6 +123,16 @@ _SIGS = {
     "rtx_shade_hits": (_i32, [_c_void_p, _i32, _i32, _c_void_p, _i64, _c_void_p, _c_void_p, _i64, _i32, _c_void_p,
                               _i32, _c_void_p, _size, _c_void_p, _c_void_p]),
     "rtx_assemble_rows": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "rtx_rccl_load": (_i32, [ctypes.c_char_p]),
+    "rtx_comm_unique_id": (_i32, [_c_void_p]),
+    "rtx_comm_init": (_i32, [_c_void_p, _i32, _i32, ctypes.POINTER(_c_void_p)]),
+    "rtx_comm_destroy": (_i32, [_c_void_p]),
+    "rtx_tiles_create": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_c_void_p),
+                                ctypes.POINTER(_c_void_p), _i64, ctypes.c_uint, ctypes.POINTER(_c_void_p)]),
+    "rtx_tiles_submit": (_i32, [_c_void_p, _i32, _c_void_p, _i32, _i32, _c_void_p, _size, ctypes.c_uint, _c_void_p,
+                                _c_void_p, _c_void_p]),
+    "rtx_tiles_finish": (_i32, [_c_void_p, _i32, _c_void_p]),
+    "rtx_tiles_destroy": (_i32, [_c_void_p]),
 }
 
 _lib = None
@@ -171,3 +193,10 @@ def stream_handle(stream=None) -> int:
     if stream is None:
         stream = torch.cuda.current_stream()
     return int(stream.cuda_stream)
+
+
+def rccl_load() -> None:
+    """Bind the row-tiled frame's RCCL calls to the librccl torch loaded (one RCCL instance per
+    process: a communicator must be driven by the library that created it)."""
+    path = Path(torch.__file__).resolve().parent / "lib" / "librccl.so"
+    check(load().rtx_rccl_load(str(path).encode() if path.exists() else None), "rtx_rccl_load")

@@ -340,15 +340,9 @@ class HipRenderer(Renderer):
         ``into``: a contiguous device tensor of that shape and dtype to render into (a
         pre-allocated gather buffer) instead of a new one. ``blob``/``n_spheres``: an already
         packed device scene (checked against its header)."""
-        cam = scene.camera
-        W, H = int(cam.width), int(cam.height)
-        key = None
-        if blob is None:
-            key = scene_key(scene)
-            blob, n_spheres = self._scene_entry(key)
-        else:
-            _check_blob(blob, n_spheres, self.device)
-        rows = n_local_rows(H, row_block, n_parts, part)
+        W = int(scene.camera.width)
+        blob, n_spheres, rows, ws, flags, probe, key = self._tile_launch(scene, row_block, n_parts, part, blob,
+                                                                         n_spheres)
         n = W * rows
         if out == "u8":
             shape, dtype, kind = (rows, W, 3), torch.uint8, L.OUT_U8_HWC
@@ -362,20 +356,49 @@ class HipRenderer(Renderer):
                 raise ValueError(f"into: need a contiguous {dtype} tensor of shape {shape} on {self.device}, got "
                                  f"{into.dtype} {tuple(into.shape)} on {into.device}")
             res = into
-        ws = self.workspace(n)
-        flags, probe = 0, None
-        capped = self.max_bounces is not None and self.max_bounces <= L.FAST_MAX_BOUNCES
-        if key is not None and capped and self.stats_buffer is None:
-            key = (key, row_block, n_parts, part, self.max_bounces)
-            flags, probe = self._general_plan(key)
-        L.check(self._lib.rtx_render_camera_ex(blob.data_ptr(), n_spheres, W, H, row_block, n_parts, part, rows,
-                                               self._bounces_arg, res.data_ptr(), kind, ws.data_ptr(), ws.numel(),
-                                               self._stats_ptr(), self._stream(), flags,
+        L.check(self._lib.rtx_render_camera_ex(blob.data_ptr(), n_spheres, W, int(scene.camera.height), row_block,
+                                               n_parts, part, rows, self._bounces_arg, res.data_ptr(), kind,
+                                               ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream(), flags,
                                                None if probe is None else probe.data_ptr()), "rtx_render_camera")
         if probe is not None:
             self._probe_landed(key, probe)
         self._check_status(ws)
         return res
+
+    def _tile_launch(self, scene, row_block, n_parts, part, blob=None, n_spheres=None):
+        """What a camera launch of one row tile needs: (blob, n_spheres, local rows, workspace, flags,
+        probe, probe key) — the scene's device blob (cached by content, or the caller's, checked),
+        and the general-kernel plan of a capped render (_general_plan)."""
+        H = int(scene.camera.height)
+        key = None
+        if blob is None:
+            key = scene_key(scene)
+            blob, n_spheres = self._scene_entry(key)
+        else:
+            _check_blob(blob, n_spheres, self.device)
+        rows = n_local_rows(H, row_block, n_parts, part)
+        ws = self.workspace(int(scene.camera.width) * rows)
+        flags, probe = 0, None
+        capped = self.max_bounces is not None and self.max_bounces <= L.FAST_MAX_BOUNCES
+        if key is not None and capped and self.stats_buffer is None:
+            key = (key, row_block, n_parts, part, self.max_bounces)
+            flags, probe = self._general_plan(key)
+        return blob, n_spheres, rows, ws, flags, probe, key
+
+    @_on_device
+    def submit_tiles(self, plan, slot: int, scene, row_block: int, n_parts: int, part: int, frame) -> None:
+        """One frame of a row-tiled plan (rtx_tiles_submit, distributed.TileGather): this rank's tile
+        of ``scene`` rendered into the plan's slot, the RCCL gather to the root and, there, the
+        assembly into ``frame`` (None on peers), all enqueued by one native call."""
+        blob, n_spheres, rows, ws, flags, probe, key = self._tile_launch(scene, row_block, n_parts, part)
+        L.check(self._lib.rtx_tiles_submit(plan, int(slot), blob.data_ptr(), n_spheres, self._bounces_arg,
+                                           ws.data_ptr(), ws.numel(), flags,
+                                           None if probe is None else probe.data_ptr(),
+                                           None if frame is None else frame.data_ptr(), self._stream()),
+                "rtx_tiles_submit")
+        if probe is not None:
+            self._probe_landed(key, probe)
+        self._check_status(ws)
 
     @_on_device
     def render_batch(self, scenes, out: str | None = None) -> torch.Tensor:

@@ -78,3 +78,61 @@ def test_nccl_two_slot_pipeline_equals_single_frames():
             assert torch.equal(one.render(frames[2]), want[2])
     finally:
         dist.destroy_process_group()
+
+
+def test_native_tiles_loopback_and_graph_replay():
+    """The native row-tiled step (rtx_tiles_submit) on a one-rank RCCL group: (1) a loopback plan —
+    the tile sent to and received from the rank itself over RCCL, then assembled — gives the
+    single-GPU frames bit for bit through the two-slot pipeline; (2) a render_tile(into=) frame and
+    a native tiles step captured into HIP graphs (include/rtx_hip.h: the entry points never
+    allocate or synchronise) replay to the eager frames bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.distributed import TileGather
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        base = scenes.random_spec(40, 2, 104, 57)
+        frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 9))) for k in range(5)]
+        r = HipRenderer(max_bounces=4, color_dtype=torch.float32, device=dev)
+        want = [r.render_tile(sc, out="u8").clone() for sc in frames]
+        tg = TileGather(r, 104, 57, row_block=8, out="u8", slots=2, loopback=True)
+        assert tg.plan is not None and tg.send and tg.recv is not None
+        got, open_slot = [], None
+        for k, sc in enumerate(frames):
+            tg.submit(sc, k % 2)
+            if open_slot is not None:
+                got.append(tg.finish(open_slot))
+            open_slot = k % 2
+        got.append(tg.finish(open_slot))
+        torch.cuda.synchronize()
+        for k in range(len(frames)):
+            assert torch.equal(got[k], want[k]), k
+
+        sc = frames[3]
+        buf = torch.empty_like(want[3])
+        r.render_tile(sc, out="u8", into=buf)  # eager first: code objects, scene upload, workspace
+        tgd = TileGather(r, 104, 57, row_block=8, out="u8", slots=1, persistent_frames=True)
+        torch.cuda.synchronize()
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            r.render_tile(sc, out="u8", into=buf)
+        with torch.cuda.graph(g2):
+            tgd.submit(sc, 0)
+            tgd.finish(0)
+        for _ in range(2):
+            buf.zero_()
+            tgd.frames[0].zero_()
+            g1.replay()
+            g2.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(buf, want[3])
+            assert torch.equal(tgd.frames[0], want[3])
+    finally:
+        dist.destroy_process_group()

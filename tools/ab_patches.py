@@ -261,8 +261,8 @@ def tile_trace(src: str) -> str:
     record counter, word 1: capacity, records from word 8). The persistent loop times each fetched
     tile; the one-tile-per-block path times the wave from kernel entry (scene staging included).
     s_memrealtime is the 100 MHz constant clock; the arithmetic of the render is unchanged."""
-    src = _sub(src, "  uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null\n};",
-               "  uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null\n"
+    src = _sub(src, "  int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred\n};",
+               "  int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred\n"
                "  unsigned long long* trace;  // tile_trace instrument\n};")
     rec = """
 __device__ __forceinline__ void trace_rec(const Params& p, unsigned long long t0, unsigned long long id) {
