@@ -305,6 +305,10 @@ def main():
                     "achieved": round(achieved_exec, 4), "frac": round(achieved_exec / PEAK_FP64_TFLOPS, 5),
                     "flops_per_launch": flops_exec, "sphere_tests": st["sphere_tests"],
                     "node_tests": st["node_tests"], "sphere_tests_reference": S * (R_tr + R_sh),
+                    "reflected_rays": {"sphere_tests": st["sphere_tests_reflected"],
+                                       "node_tests": st["node_tests_reflected"],
+                                       "beam_searches": st["beam_searches"],
+                                       "wave_searches": sum(st["waves_traced"][1:])},
                     "note": "15/primary ray + 20/ray-sphere test + 22/culling-node test + 200/shaded hit over the "
                             "tests k_render_fast executed (kernel counters); `achieved` above prices every test the "
                             "reference performs (S per ray), culled or not"},
@@ -447,6 +451,23 @@ def secondary_tiles(args, r, scene, world, dev, coll_dev):
                            "ms_per_step": round(t / k4 * 1e3, 5), "steps": k4, "scaling": "strong",
                            "config": "C4: 64 random spheres + ground 7680x4320 seed 0, 5 bounces, row-tiled over "
                                      f"{world} rank(s), gather of the uint8 frame to rank 0"}
+        if world > 1:
+            # the strong-scaling speed-up in the same run: rank 0 alone renders the whole C4 frame
+            # as the one-rank tiles path does (straight into the uint8 frame), the others wait
+            if dist.get_rank() == 0:
+                c4 = scenes.build_scene(c4spec)
+                buf = torch.empty((4320, 7680, 3), dtype=torch.uint8, device=dev)
+                for _ in range(2):
+                    r4.render_tile(c4, out="u8", into=buf)
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(k4):
+                    r4.render_tile(c4, out="u8", into=buf)
+                torch.cuda.synchronize(dev)
+                t1 = (time.perf_counter() - t0) / k4
+                out["c4_tiles"]["single_gpu_ms_per_step"] = round(t1 * 1e3, 5)
+                out["c4_tiles"]["speedup_vs_1gpu"] = round(t1 / (t / k4), 4)
+            dist.barrier()
     except Exception as e:  # noqa: BLE001
         out["tiles_error"] = repr(e)[:300]
     finally:

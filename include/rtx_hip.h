@@ -184,6 +184,9 @@ enum {
   RTX_S_TIES = 2,     /* (ray, level) pairs with >1 nearest shape */
   RTX_S_TESTS = 3,    /* ray-sphere tests executed by live lanes (fast kernel; culling skips most) */
   RTX_S_NODES = 4,    /* culling-node (box) tests executed by live lanes (fast kernel)            */
+  RTX_S_TESTS1 = 5,   /* ... of them, the sphere tests of reflected rays' nearest-hit searches (levels >= 1) */
+  RTX_S_NODES1 = 6,   /* ... and their node tests (beam plane tests priced as two node tests a pass) */
+  RTX_S_BEAMW = 7,    /* reflected-ray searches served by the wave's beam candidates (waves x levels) */
   RTX_S_LEVELS = 64,  /* levels recorded                        */
   RTX_S_RAYS = 8,     /* [8 .. 8+64): rays traced per level     */
   RTX_S_HITS = 72,    /* [72 .. 72+64): shaded hits (= shadow rays) per level */

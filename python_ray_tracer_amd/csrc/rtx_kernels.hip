@@ -513,6 +513,7 @@ struct Work {
 template <>
 struct Work<true> {
   uint32_t tests = 0, nodes = 0;
+  uint32_t tests1 = 0, nodes1 = 0;  // of the nearest-hit searches of reflected rays (levels >= 1)
   __device__ __forceinline__ void test(int k) { tests += (uint32_t)k; }
   __device__ __forceinline__ void node() { ++nodes; }
 };
@@ -1779,11 +1780,17 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_add(st, RTX_S_RAYS + kb + k + 1, 1);
       stat_wave(st, RTX_S_WTRACE + kb + k + 1);
     }
+    [[maybe_unused]] uint32_t tests0 = 0, nodes0 = 0;
+    if constexpr (STATS) {
+      tests0 = wk.tests;
+      nodes0 = wk.nodes;
+    }
     if (TREE && sc[RTX_H_NNODES] != 0.0) {
       // the wave's beam candidates (tame scenes up to 128 spheres), else the culling tree
       Beam bm;
       const double* btab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
       if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(btab, nsph, ox, oy, oz, dx, dy, dz, bm)) {
+        if (st) stat_wave(st, RTX_S_BEAMW);
         for (int j = 0; j < bm.passes; ++j) {  // a lane's sphere test per pass, priced as two node tests
           wk.node();                            // (like wave_frustum)
           wk.node();
@@ -1797,12 +1804,18 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     } else {
       nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
     }
+    if constexpr (STATS) {
+      wk.tests1 += wk.tests - tests0;
+      wk.nodes1 += wk.nodes - nodes0;
+    }
   }
 
   if constexpr (STATS) {
     if (st) {
       stat_add(st, RTX_S_TESTS, wk.tests);
       stat_add(st, RTX_S_NODES, wk.nodes);
+      stat_add(st, RTX_S_TESTS1, wk.tests1);
+      stat_add(st, RTX_S_NODES1, wk.nodes1);
     }
   }
   if (deferred) {

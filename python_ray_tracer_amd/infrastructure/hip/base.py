@@ -589,6 +589,8 @@ class HipRenderer(Renderer):
         last = max([i + 1 for i, v in enumerate(rays) if v] or [0])
         return {"pixels": s[L.S_PIXELS], "deferred": s[L.S_DEFERRED], "ties": s[L.S_TIES],
                 "sphere_tests": s[L.S_TESTS], "node_tests": s[L.S_NODES],
+                "sphere_tests_reflected": s[L.S_TESTS1], "node_tests_reflected": s[L.S_NODES1],
+                "beam_searches": s[L.S_BEAMW],
                 "rays": rays[:last], "hits": hits[:last],
                 "waves_traced": s[L.S_WTRACE:L.S_WTRACE + last], "waves_shaded": s[L.S_WSHADE:L.S_WSHADE + last]}
 
