@@ -257,20 +257,23 @@ TRACE_WORDS = 4  # per record: t_start, t_end (s_memrealtime, 100 MHz), tile id,
 
 def tile_trace(src: str) -> str:
     """Per-tile timestamps of k_render_fast: every wave records (start, end, tile, hardware id) of
-    each tile it renders into a device buffer registered with ``rtx_trace_set(buf)`` (word 0: the
-    record counter, word 1: capacity, records from word 8). The persistent loop times each fetched
-    tile; the one-tile-per-block path times the wave from kernel entry (scene staging included).
+    each tile it renders into a device buffer registered with ``rtx_trace_set(buf)`` (word 1: capacity,
+    records from word 8, record k = tile k / wave k of the launch; an unrendered slot stays 0). The
+    persistent loop times each fetched tile; the one-tile-per-block path times the wave from kernel entry (scene staging included).
     s_memrealtime is the 100 MHz constant clock; the arithmetic of the render is unchanged."""
     src = _sub(src, "  int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred\n};",
                "  int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred\n"
                "  unsigned long long* trace;  // tile_trace instrument\n};")
     rec = """
-__device__ __forceinline__ void trace_rec(const Params& p, unsigned long long t0, unsigned long long id) {
+__device__ __forceinline__ void trace_rec(const Params& p, unsigned long long t0, unsigned long long id,
+                                          unsigned long long slot) {
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   if (p.trace && (threadIdx.x & 63) == 0) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
-    const unsigned long long k = atomicAdd(p.trace, 1ull);
+    // one record per tile at its own slot: no shared counter (a global atomic per tile serialised
+    // the traced launch across XCDs, ~50 ns per record, 14x the untraced C4 kernel)
+    const unsigned long long k = slot;
     if (k < p.trace[1]) {
       unsigned long long* r = p.trace + 8 + 4 * k;
       r[0] = t0; r[1] = t1; r[2] = id; r[3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
@@ -286,10 +289,11 @@ __device__ __forceinline__ void trace_rec(const Params& p, unsigned long long t0
     old = ("      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, "
            "false, lds_tab, true);\n")
     src = _sub(src, old, "      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();\n" + old +
-               "      trace_rec(p, t0, (unsigned long long)t | ((unsigned long long)pw << 32));\n")
+               "      trace_rec(p, t0, (unsigned long long)t | ((unsigned long long)pw << 32), (unsigned long long)t);\n")
     old = "  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);\n}"
     src = _sub(src, old, old[:-1] + "  trace_rec(p, t_entry, ((unsigned long long)(blockIdx.y * gridDim.x + blockIdx.x) * "
-               "kFastWaves + (threadIdx.x >> 6)) | (1ull << 63));\n}")
+               "kFastWaves + (threadIdx.x >> 6)) | (1ull << 63), (unsigned long long)(blockIdx.y * gridDim.x + "
+               "blockIdx.x) * kFastWaves + (threadIdx.x >> 6));\n}")
     src = _sub(src, "int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {\n",
                "unsigned long long* g_trace = nullptr;\n"
                "int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {\n"

@@ -68,6 +68,8 @@ def source_functions(path: Path):
                          r"dim3|WsLayout|int64_t|inline|constexpr)\b.*?\b(\w+)\s*\(", line)
             if m and not line.rstrip().endswith(";"):
                 start, name = i, m.group(1)
+        if re.match(r"^(namespace\b.*\{|\}\s*//\s*namespace|extern \"C\" \{|\}\s*//\s*extern)", line):
+            continue  # namespace / extern "C" braces do not nest functions
         depth += line.count("{") - line.count("}")
         if start is not None and depth == 0 and "{" in "".join(lines[start - 1:i]):
             out.append((start, i, name))
@@ -126,6 +128,14 @@ def main(asm_path: str, symbol: str) -> None:
     by_func = defaultdict(Counter)
     by_line = defaultdict(Counter)
     meta = {}
+    # the .file index of rtx_kernels.hip (0 when it is the compiled unit; rtx_small.hip includes it)
+    kfile = "0"
+    with open(asm_path) as f:
+        for raw in f:
+            m = re.match(r'\s*\.file\s+(\d+)\s+"[^"]*"(?:\s+"([^"]*)")?', raw)
+            if m and (m.group(2) or "").endswith(SRC.name) or (m and m.group(2) is None and SRC.name in raw):
+                kfile = m.group(1)
+                break
     inside = False
     cur = ("?", 0)
     with open(asm_path) as f:
@@ -145,7 +155,7 @@ def main(asm_path: str, symbol: str) -> None:
                 continue
             op = s.split()[0]
             c = classify(op)
-            key = func_of(cur[1]) if cur[0] == "0" else f"hdr{cur[0]}"
+            key = func_of(cur[1]) if cur[0] == kfile else f"hdr{cur[0]}"
             by_func[key][c] += 1
             by_line[cur][c] += 1
     # kernel resource metadata (the .amdhsa block after the function)
@@ -174,9 +184,9 @@ def main(asm_path: str, symbol: str) -> None:
     for name, c in sorted(by_func.items(), key=lambda kv: -sum(kv[1].values())):
         print(f"{name:28s}" + "".join(f"{c[k]:10d}" for k in CLASSES) + f"{sum(c.values()):8d}")
     print(f"{'TOTAL':28s}" + "".join(f"{total[k]:10d}" for k in CLASSES) + f"{sum(total.values()):8d}")
-    print("\ntop source lines (file 0 = rtx_kernels.hip):")
+    print(f"\ntop source lines (file {kfile} = rtx_kernels.hip):")
     for (fi, ln), c in sorted(by_line.items(), key=lambda kv: -sum(kv[1].values()))[:40]:
-        src = SRC.read_text().splitlines()[ln - 1].strip()[:70] if fi == "0" and ln > 0 else ""
+        src = SRC.read_text().splitlines()[ln - 1].strip()[:70] if fi == kfile and ln > 0 else ""
         print(f"  {fi}:{ln:5d} {sum(c.values()):5d}  {dict(c.most_common(4))}  {src}")
 
 

@@ -158,8 +158,9 @@ def main():
         launch()
         lib.rtx_trace_set(None)
         torch.cuda.synchronize()
-        cnt = int(buf[0].item())
-        rec = buf[8:8 + WORDS * min(cnt, cap)].view(-1, WORDS).cpu().numpy().view(np.uint64)
+        rec = buf[8:8 + WORDS * cap].view(-1, WORDS).cpu().numpy().view(np.uint64)
+        rec = rec[rec[:, 1] != 0]  # the slots of rendered tiles / waves
+        cnt = len(rec)
         r, dur, t0 = analyse(rec, persistent, (W + 7) // 8)
         r["records"] = cnt
         res.append(r)
