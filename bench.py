@@ -76,6 +76,12 @@ def parse():
                     help="one GPU: time every part p of render_tile(scene, row_block, N, p) for each N (the compute "
                          "side of the N-GPU row-tiled frame) and assemble_rows of N parts; prints one JSON line "
                          "(metric: per-part kernel time) instead of the bench line")
+    ap.add_argument("--no-tile-order", action="store_true",
+                    help="persistent launches (>= 32 spheres) keep the bottom-up wave-tile order instead of the "
+                         "longest-first order HipRenderer learns from its first launch (A/B)")
+    ap.add_argument("--no-octant-tree", action="store_true",
+                    help="pack the culling tree in one layout instead of one nearest-first layout per ray "
+                         "direction octant (A/B)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -113,13 +119,17 @@ def main():
             dist.init_process_group("gloo")
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
+    if args.no_octant_tree:
+        from python_ray_tracer_amd.infrastructure.hip import scene_pack
+
+        scene_pack.BVH_OCTANT_LAYOUTS = False
     spec, B = scenes.CONFIGS[args.config]()
     if args.bounces is not None:
         B = None if args.bounces < 0 else args.bounces
     W, H = spec["camera"]["width"], spec["camera"]["height"]
     scene = scenes.build_scene(spec)
     dtype = torch.float64 if args.out == "f64" else torch.float32
-    r = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev)
+    r = HipRenderer(max_bounces=B, color_dtype=dtype, device=dev, learn_tile_order=not args.no_tile_order)
 
     if args.emulate_parts:
         line = emulate_parts(args, r, scene, spec, B, [int(v) for v in args.emulate_parts.split(",")])
@@ -443,7 +453,8 @@ def secondary_tiles(args, r, scene, world, dev, coll_dev):
                                      f"into the gather buffer (row_block {args.row_block}), gather to rank 0, "
                                      "rtx_assemble_rows, uint8 frame, two frames in flight"}
         c4spec, c4B = scenes.CONFIGS["C4"]()
-        r4 = HipRenderer(max_bounces=c4B, color_dtype=torch.float32, device=dev)
+        r4 = HipRenderer(max_bounces=c4B, color_dtype=torch.float32, device=dev,
+                         learn_tile_order=not args.no_tile_order)
         step, drain = tiles_stepper(r4, scenes.build_scene(c4spec), world, args.row_block, "u8")
         k4 = 10
         t = timed(step, drain, k4, 2)

@@ -177,6 +177,10 @@ struct Params {
   int frame;  // set per block / per deferred ray (kernel side)
   uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null
   int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred
+  // persistent launches (rtx_render_camera_sched): the wave tiles in dispatch order (null: bottom-up
+  // row order), and per-tile render times to record (s_memrealtime ticks), or null
+  const uint32_t* tile_order;
+  uint32_t* tile_cost;
 };
 
 // Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
@@ -592,6 +596,21 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
   }
 }
 
+// The culling tree's node array for the wave's rays: the nearest-first layout of the wave's majority
+// direction octant when the packer stored all eight (RTX_H_NODEOCT), else the single layout. Any
+// layout visits the same nodes under the same test; nearest-first finds near hits early, so the far
+// subtrees fail their node test against the shorter t_nearest (or, for shadow rays, an occluder ends
+// the walk sooner).
+__device__ __forceinline__ const cdouble* tree_nodes(const cdouble* sc, double dx, double dy, double dz) {
+  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
+  if (sc[RTX_H_NODEOCT] == 0.0) return nodes;
+  const int n = __builtin_popcountll(__ballot(1));
+  const int o = (2 * __builtin_popcountll(__ballot(dx < 0.0)) > n ? 1 : 0) |
+                (2 * __builtin_popcountll(__ballot(dy < 0.0)) > n ? 2 : 0) |
+                (2 * __builtin_popcountll(__ballot(dz < 0.0)) > n ? 4 : 0);
+  return nodes + o * (int)sc[RTX_H_NNODES] * RTX_NODE_WORDS;
+}
+
 // Nearest hit through the culling tree: the always-tested spheres, then a stackless depth-first
 // walk that enters a node when any lane of the wave may hit it before its current nearest t.
 // Evaluation order differs from scene order, which the result does not depend on: the nearest t
@@ -600,7 +619,7 @@ template <bool CAM, typename Wk>
 __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double oy, double oz, double dx, double dy,
                                             double dz, double& tmin, int& hit, bool& tie, double tame, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
-  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
+  const cdouble* nodes = tree_nodes(sc, dx, dy, dz);
   const int nn = (int)sc[RTX_H_NNODES];
   const double oo = dot3(ox, oy, oz, ox, oy, oz);
   tmin = FARAWAY;
@@ -675,7 +694,7 @@ template <typename Wk>
 __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
                                         double ly, double lz, double tself, int hs, double tame, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
-  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
+  const cdouble* nodes = tree_nodes(sc, lx, ly, lz);
   const int nn = (int)sc[RTX_H_NNODES];
   const int nal = (int)sc[RTX_H_NALWAYS];
   bool lit = true;
@@ -1927,10 +1946,16 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
     if (lane == 0) nxt = atomicAdd(ctr, 1u);
     int k = pw / nc;
     int v = 0;
+    // the host's dispatch order (longest tiles first, learnt from an earlier launch's tile_cost), read
+    // through the scalar cache: the index is wave-uniform
+    const uint32_t __attribute__((address_space(4)))* const order =
+        (const uint32_t __attribute__((address_space(4)))*)p.tile_order;
     while (k < tiles_c) {
-      const int t = c + k * nc;
+      const int t = order ? (int)order[c + k * nc] : c + k * nc;
       const int row = t / p.n_tiles_x;
+      const uint64_t tc0 = p.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;
       fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
+      if (p.tile_cost && lane == 0) p.tile_cost[t] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc0);
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
       if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
@@ -2655,10 +2680,27 @@ size_t rtx_workspace_bytes(int64_t n_rays, int max_bounces) {
   return ws_bytes(n_rays, max_bounces);
 }
 
+int rtx_wave_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles) {
+  if (!n_tiles) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  *n_tiles = n_spheres >= kPersistMinSpheres && width > 0 && n_local_rows > 0
+                 ? (int64_t)((width + kWaveW - 1) / kWaveW) * ((n_local_rows + kWaveH - 1) / kWaveH)
+                 : 0;
+  return RTX_OK;
+}
+
 int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
                          int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
                          size_t workspace_bytes, uint64_t* stats, void* stream, unsigned flags,
                          uint32_t* deferred_out) {
+  return rtx_render_camera_sched(scene, n_spheres, width, height, row_block, n_parts, part, n_local_rows,
+                                 max_bounces, out, out_kind, workspace, workspace_bytes, stats, stream, flags,
+                                 deferred_out, nullptr, nullptr);
+}
+
+int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
+                            int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
+                            size_t workspace_bytes, uint64_t* stats, void* stream, unsigned flags,
+                            uint32_t* deferred_out, const uint32_t* tile_order, uint32_t* tile_cost) {
   if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
       n_local_rows < 0 || n_local_rows > height)
     return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
@@ -2679,6 +2721,8 @@ int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int heig
   p.out_kind = out_kind;
   p.stats = (unsigned long long*)stats;
   p.deferred_out = deferred_out;
+  p.tile_order = tile_order;  // used by the persistent launch only (rtx_wave_tiles > 0)
+  p.tile_cost = tile_cost;
   return run_render(p, workspace, workspace_bytes, (hipStream_t)stream, (flags & RTX_F_NO_GENERAL) != 0);
 }
 

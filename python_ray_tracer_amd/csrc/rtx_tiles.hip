@@ -200,15 +200,19 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
 }
 
 int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, int max_bounces, void* workspace,
-                     size_t workspace_bytes, unsigned flags, uint32_t* deferred_out, void* frame, void* stream) {
+                     size_t workspace_bytes, unsigned flags, uint32_t* deferred_out, const uint32_t* tile_order,
+                     uint32_t* tile_cost, void* frame, void* stream) {
   Tiles* t = (Tiles*)plan;
   if (!t) return err(RTX_E_ARG, "null plan%s", "");
   if (slot < 0 || slot >= t->slots) return err(RTX_E_ARG, "bad slot%s (%lld)", "", slot);
   hipStream_t s = (hipStream_t)stream;
   const bool root = t->rank == t->root;
   if (root && !frame) return err(RTX_E_ARG, "the root needs a frame buffer%s", "");
+  // a one-rank plan without loopback renders straight into the caller's frame on the caller's
+  // stream: stream order is all the ordering it needs (no event: each costs the stream a barrier)
+  const bool direct = t->world == 1 && !t->loop;
   // the slot's buffers are free once its previous frame's gather and assembly have run
-  if (t->used[slot]) {
+  if (t->used[slot] && !direct) {
     if (hipError_t e = hipStreamWaitEvent(s, t->done[slot], 0))
       return err(RTX_E_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
@@ -218,14 +222,11 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
               : t->world == 1 ? frame
               : root          ? (uint8_t*)t->recv[slot] + (int64_t)t->root * t->part_bytes
                               : t->send[slot];
-  if (int rc = rtx_render_camera_ex(scene, n_spheres, t->width, t->height, t->row_block, t->world, t->rank,
-                                    t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes, nullptr,
-                                    stream, flags, deferred_out))
+  if (int rc = rtx_render_camera_sched(scene, n_spheres, t->width, t->height, t->row_block, t->world, t->rank,
+                                       t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes,
+                                       nullptr, stream, flags, deferred_out, tile_order, tile_cost))
     return rc;
-  if (t->world == 1 && !t->loop) {
-    if (hipError_t e = hipEventRecord(t->done[slot], s)) return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
-    return RTX_OK;
-  }
+  if (direct) return RTX_OK;
   hipError_t e = hipEventRecord(t->rendered[slot], s);
   if (e == hipSuccess) e = hipStreamWaitEvent(t->cs, t->rendered[slot], 0);
   if (e != hipSuccess) return err(RTX_E_LAUNCH, "event: %s", hipGetErrorString(e));
@@ -259,7 +260,7 @@ int rtx_tiles_finish(void* plan, int slot, void* stream) {
   Tiles* t = (Tiles*)plan;
   if (!t) return err(RTX_E_ARG, "null plan%s", "");
   if (slot < 0 || slot >= t->slots) return err(RTX_E_ARG, "bad slot%s (%lld)", "", slot);
-  if (!t->used[slot]) return RTX_OK;
+  if (!t->used[slot] || (t->world == 1 && !t->loop)) return RTX_OK;  // direct: in stream order already
   if (hipError_t e = hipStreamWaitEvent((hipStream_t)stream, t->done[slot], 0))
     return err(RTX_E_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
   return RTX_OK;

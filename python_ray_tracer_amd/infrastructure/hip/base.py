@@ -23,6 +23,7 @@ Differences from the reference, all deliberate and documented in DESIGN.md:
 
 from __future__ import annotations
 
+import ctypes
 import numbers
 import os
 from pathlib import Path
@@ -212,7 +213,7 @@ class HipRenderer(Renderer):
     """MI355X renderer behind the reference ``Renderer`` plugin surface (application.py:7-32)."""
 
     def __init__(self, max_bounces: int | None = None, *, color_dtype: torch.dtype = torch.float64,
-                 device=None, collect_stats: bool = False) -> None:
+                 device=None, collect_stats: bool = False, learn_tile_order: bool = True) -> None:
         self._lib = L.load()
         if not torch.cuda.is_available():
             raise RuntimeError("HipRenderer needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")
@@ -226,6 +227,9 @@ class HipRenderer(Renderer):
         self._scene_cache: dict = {}
         # capped camera renders known to defer no ray (or probing): see _general_plan
         self._defers: dict = {}
+        # persistent launches: the wave-tile dispatch order learnt per (scene, tile, cap), see _sched_plan
+        self.learn_tile_order = bool(learn_tile_order)
+        self._sched: dict = {}
         self._ws = None
         self.stats_buffer = torch.zeros(L.S_WORDS, dtype=torch.int64, device=self.device) if collect_stats else None
 
@@ -341,8 +345,8 @@ class HipRenderer(Renderer):
         pre-allocated gather buffer) instead of a new one. ``blob``/``n_spheres``: an already
         packed device scene (checked against its header)."""
         W = int(scene.camera.width)
-        blob, n_spheres, rows, ws, flags, probe, key = self._tile_launch(scene, row_block, n_parts, part, blob,
-                                                                         n_spheres)
+        blob, n_spheres, rows, ws, flags, probe, key, order, cost = self._tile_launch(scene, row_block, n_parts, part,
+                                                                                      blob, n_spheres)
         n = W * rows
         if out == "u8":
             shape, dtype, kind = (rows, W, 3), torch.uint8, L.OUT_U8_HWC
@@ -356,19 +360,25 @@ class HipRenderer(Renderer):
                 raise ValueError(f"into: need a contiguous {dtype} tensor of shape {shape} on {self.device}, got "
                                  f"{into.dtype} {tuple(into.shape)} on {into.device}")
             res = into
-        L.check(self._lib.rtx_render_camera_ex(blob.data_ptr(), n_spheres, W, int(scene.camera.height), row_block,
-                                               n_parts, part, rows, self._bounces_arg, res.data_ptr(), kind,
-                                               ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream(), flags,
-                                               None if probe is None else probe.data_ptr()), "rtx_render_camera")
-        if probe is not None:
-            self._probe_landed(key, probe)
+        L.check(self._lib.rtx_render_camera_sched(blob.data_ptr(), n_spheres, W, int(scene.camera.height), row_block,
+                                                  n_parts, part, rows, self._bounces_arg, res.data_ptr(), kind,
+                                                  ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream(), flags,
+                                                  _ptr(probe), _ptr(order), _ptr(cost)), "rtx_render_camera")
+        self._after_launch(key, probe, cost)
         self._check_status(ws)
         return res
 
+    def _after_launch(self, key, probe, cost) -> None:
+        if probe is not None:
+            self._probe_landed(key, probe)
+        if cost is not None:
+            self._cost_landed(key, cost)
+
     def _tile_launch(self, scene, row_block, n_parts, part, blob=None, n_spheres=None):
         """What a camera launch of one row tile needs: (blob, n_spheres, local rows, workspace, flags,
-        probe, probe key) — the scene's device blob (cached by content, or the caller's, checked),
-        and the general-kernel plan of a capped render (_general_plan)."""
+        probe, key, tile order, tile cost) — the scene's device blob (cached by content, or the
+        caller's, checked), the general-kernel plan of a capped render (_general_plan) and the
+        persistent launch's dispatch order (_sched_plan)."""
         H = int(scene.camera.height)
         key = None
         if blob is None:
@@ -378,26 +388,62 @@ class HipRenderer(Renderer):
             _check_blob(blob, n_spheres, self.device)
         rows = n_local_rows(H, row_block, n_parts, part)
         ws = self.workspace(int(scene.camera.width) * rows)
-        flags, probe = 0, None
+        flags, probe, order, cost = 0, None, None, None
         capped = self.max_bounces is not None and self.max_bounces <= L.FAST_MAX_BOUNCES
-        if key is not None and capped and self.stats_buffer is None:
+        if key is not None and self.stats_buffer is None:
             key = (key, row_block, n_parts, part, self.max_bounces)
-            flags, probe = self._general_plan(key)
-        return blob, n_spheres, rows, ws, flags, probe, key
+            if capped:
+                flags, probe = self._general_plan(key)
+            if self.learn_tile_order:
+                order, cost = self._sched_plan(key, int(scene.camera.width), rows, n_spheres)
+        return blob, n_spheres, rows, ws, flags, probe, key, order, cost
+
+    def _sched_plan(self, key, width, rows, n_spheres):
+        """(tile_order, tile_cost) of a persistent launch (rtx_render_camera_sched; scenes of >= 32
+        spheres). A few wave tiles with long reflection chains can run alone at the end of the
+        launch; handing the longest tiles out first removes that drain. The render is deterministic
+        (same blob content, tile and cap: the same rays), so the first launch of a key records every
+        tile's render time (tile_cost, copied to pinned memory behind an event, nothing waits) and,
+        once it has landed, later launches of the key pass the tiles in descending cost order. Output
+        does not depend on the order."""
+        st = self._sched.get(key)
+        if st is not None and st[0] == "order":
+            return st[1], None
+        if torch.cuda.is_current_stream_capturing():
+            return None, None
+        if st is not None:  # ("cost", event, pinned host copy)
+            if not st[1].query():
+                return None, None
+            order = np.argsort(-st[2].numpy().astype(np.int64), kind="stable").astype(np.int32)
+            dev = torch.from_numpy(order).pin_memory().to(self.device, non_blocking=True)
+            self._sched[key] = ("order", dev)
+            return dev, None
+        nt = ctypes.c_int64()
+        L.check(self._lib.rtx_wave_tiles(width, rows, n_spheres, ctypes.byref(nt)), "rtx_wave_tiles")
+        if nt.value <= 0:
+            self._sched[key] = ("order", None)  # not a persistent launch: nothing to order
+            return None, None
+        if len(self._sched) >= 64:
+            self._sched.pop(next(iter(self._sched)))
+        return None, torch.zeros(nt.value, dtype=torch.int32, device=self.device)
+
+    def _cost_landed(self, key, cost) -> None:
+        host = torch.empty(cost.shape, dtype=torch.int32, pin_memory=True)
+        host.copy_(cost, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._sched[key] = ("cost", ev, host)
 
     @_on_device
     def submit_tiles(self, plan, slot: int, scene, row_block: int, n_parts: int, part: int, frame) -> None:
         """One frame of a row-tiled plan (rtx_tiles_submit, distributed.TileGather): this rank's tile
         of ``scene`` rendered into the plan's slot, the RCCL gather to the root and, there, the
         assembly into ``frame`` (None on peers), all enqueued by one native call."""
-        blob, n_spheres, rows, ws, flags, probe, key = self._tile_launch(scene, row_block, n_parts, part)
+        blob, n_spheres, rows, ws, flags, probe, key, order, cost = self._tile_launch(scene, row_block, n_parts, part)
         L.check(self._lib.rtx_tiles_submit(plan, int(slot), blob.data_ptr(), n_spheres, self._bounces_arg,
-                                           ws.data_ptr(), ws.numel(), flags,
-                                           None if probe is None else probe.data_ptr(),
-                                           None if frame is None else frame.data_ptr(), self._stream()),
-                "rtx_tiles_submit")
-        if probe is not None:
-            self._probe_landed(key, probe)
+                                           ws.data_ptr(), ws.numel(), flags, _ptr(probe), _ptr(order), _ptr(cost),
+                                           _ptr(frame), self._stream()), "rtx_tiles_submit")
+        self._after_launch(key, probe, cost)
         self._check_status(ws)
 
     @_on_device
@@ -597,6 +643,10 @@ class HipRenderer(Renderer):
     def reset_stats(self) -> None:
         if self.stats_buffer is not None:
             self.stats_buffer.zero_()
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
 
 
 def _resolve_device(device) -> torch.device:

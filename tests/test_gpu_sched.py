@@ -1,0 +1,51 @@
+"""Longest-first dispatch of the persistent launch (rtx_render_camera_sched, HipRenderer._sched_plan).
+
+A scene of >= 32 spheres renders as persistent waves fetching 8x8 wave tiles. HipRenderer records
+every tile's render time on the first launch of a (scene, tile, cap) and hands the tiles out
+longest first from then on. The order changes when a tile is rendered, never what it renders: the
+frames must equal those of a renderer that keeps the bottom-up order, bit for bit, and the oracle.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def test_learnt_order_leaves_frames_unchanged():
+    dev = _dev()
+    from oracle import numpy_oracle as O
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    spec = scenes.random_spec(40, 7, 200, 131)
+    scene = scenes.build_scene(spec)
+    for B in (3, 5, None):
+        plain = HipRenderer(max_bounces=B, color_dtype=torch.float64, device=dev, learn_tile_order=False)
+        learn = HipRenderer(max_bounces=B, color_dtype=torch.float64, device=dev)
+        want = plain.render_tile(scene)
+        for rb, parts, part in ((1, 1, 0), (8, 3, 1)):
+            ref = plain.render_tile(scene, rb, parts, part)
+            got = [learn.render_tile(scene, rb, parts, part).clone() for _ in range(4)]
+            torch.cuda.synchronize()
+            got.append(learn.render_tile(scene, rb, parts, part))
+            states = [v[0] for v in learn._sched.values()]
+            assert "order" in states, states
+            for g in got:
+                assert torch.equal(g, ref), (B, rb, parts, part)
+        # the learnt order is a permutation of the wave tiles
+        for st in learn._sched.values():
+            if st[0] == "order" and st[1] is not None:
+                o = st[1].cpu().numpy()
+                assert np.array_equal(np.sort(o), np.arange(len(o)))
+        if B == 3:
+            ora = O.render(O.scene_from_spec(spec), 3)
+            assert float(np.abs(learn.render_tile(scene).cpu().numpy() - ora).max()) <= 1e-12
+            assert torch.equal(learn.render_tile(scene), want)
