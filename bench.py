@@ -77,11 +77,8 @@ def parse():
                          "side of the N-GPU row-tiled frame) and assemble_rows of N parts; prints one JSON line "
                          "(metric: per-part kernel time) instead of the bench line")
     ap.add_argument("--no-tile-order", action="store_true",
-                    help="persistent launches (>= 32 spheres) keep the bottom-up wave-tile order instead of the "
-                         "longest-first order HipRenderer learns from its first launch (A/B)")
-    ap.add_argument("--no-octant-tree", action="store_true",
-                    help="pack the culling tree in one layout instead of one nearest-first layout per ray "
-                         "direction octant (A/B)")
+                    help="camera launches keep the bottom-up tile order instead of the longest-first order "
+                         "HipRenderer learns from its first launch of a scene (A/B)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -119,10 +116,6 @@ def main():
             dist.init_process_group("gloo")
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
-    if args.no_octant_tree:
-        from python_ray_tracer_amd.infrastructure.hip import scene_pack
-
-        scene_pack.BVH_OCTANT_LAYOUTS = False
     spec, B = scenes.CONFIGS[args.config]()
     if args.bounces is not None:
         B = None if args.bounces < 0 else args.bounces

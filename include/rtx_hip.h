@@ -99,13 +99,9 @@ enum {
                         mask k set unless sphere 64k+j provably cannot shadow (shader.py:126-128 in its
                         any-hit form) a shadow ray whose nudged origin lies in the voxel; last, the
                         huge spheres' mask (rays outside the grid that miss the ball) */
-  RTX_H_SINRED = 40, /* 1: every material's thin-film phase (shader.py:208, |phase| <= 10 pi |thickness|)
+  RTX_H_SINRED = 40  /* 1: every material's thin-film phase (shader.py:208, |phase| <= 10 pi |thickness|)
                         lies in the kernel sine's reduction range (|x| <= 2^20), so no lane needs a
                         range check; 0: checked per wave */
-  RTX_H_NODEOCT = 41 /* 1: the culling tree is stored 8 times (RTX_H_NNODES nodes each, from RTX_H_NODES):
-                        layout o (bit 0/1/2 = the ray's x/y/z direction negative) lists every inner
-                        node's children nearest-first for such a ray (the child on the low side of the
-                        split first when the component is positive); 0: one layout */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 #define RTX_SHGRID_WORDS 13 /* words of the shadow-grid record before its masks */
@@ -133,8 +129,7 @@ enum {
   RTX_N_FIRST = 6,  /* leaf: first culled-geometry entry   */
   RTX_N_COUNT = 7,  /* leaf: sphere count (0: inner node)  */
   RTX_N_SKIP = 8,   /* node index after this subtree        */
-  RTX_N_MARGIN = 9, /* 2e-7 * (3 (|Cn|+R)^2 + R^2 + 1), Cn/R: the box's bounding sphere (error budget) */
-  RTX_N_AXIS = 10   /* inner node: the axis its children were split along (informational) */
+  RTX_N_MARGIN = 9  /* 2e-7 * (3 (|Cn|+R)^2 + R^2 + 1), Cn/R: the box's bounding sphere (error budget) */
 };
 
 /* per-sphere material words (NumpyShader, shader.py:36-54; derived constants computed on the
@@ -262,17 +257,19 @@ int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int heig
                          void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream,
                          unsigned flags, uint32_t* deferred_out);
 
-/* rtx_render_camera_ex with a dispatch order for the persistent launch, which renders single frames
- * (or row tiles) of scenes with >= 32 spheres as kWaveW x kWaveH (8 x 8) wave tiles that persistent
- * waves fetch from counters; rtx_wave_tiles gives their count (0: the launch is not persistent, and
- * both arrays below are ignored). Tile t is column t % tiles_x, row t / tiles_x counted from the
- * bottom of the (local) frame; the default order is t = 0, 1, 2, ... (bottom-up rows).
- *  - tile_order (may be NULL): a permutation of the tiles, the order in which they are handed out;
- *    longest tiles first shortens the launch's drain, where a few long tiles (long reflection chains)
+/* rtx_render_camera_ex with a dispatch order. A camera launch of one frame (or row tile) is
+ * dispatched in units: scenes of >= 32 spheres run persistent waves fetching kWaveW x kWaveH (8 x 8)
+ * wave tiles from counters; smaller scenes one block tile (4 waves) per block, blocks dispatched in
+ * grid order. rtx_sched_tiles gives the number of units; unit t is column t % units_x, row
+ * t / units_x counted from the bottom of the (local) frame, and the default order is t = 0, 1, 2, ...
+ * (bottom-up rows: the ground and the spheres, whose pixels run long bounce chains, first).
+ *  - tile_order (may be NULL): a permutation of the units, the order in which they are handed out.
+ *    Longest first shortens the launch's drain, where a few long units (long reflection chains)
  *    would otherwise run alone at its end. Output does not depend on the order.
- *  - tile_cost (may be NULL): receives each tile's render time (s_memrealtime ticks, 100 MHz) of this
- *    launch, from which a caller derives the order of the next identical launch. */
-int rtx_wave_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles);
+ *  - tile_cost (may be NULL; zero-filled): receives each unit's render time (s_memrealtime ticks,
+ *    100 MHz; a block tile: its slowest wave) in this launch, from which a caller derives the order
+ *    of the next identical launch. */
+int rtx_sched_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles);
 int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int height,
                             int row_block, int n_parts, int part, int n_local_rows,
                             int max_bounces, void* out, int out_kind,

@@ -177,8 +177,9 @@ struct Params {
   int frame;  // set per block / per deferred ray (kernel side)
   uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null
   int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred
-  // persistent launches (rtx_render_camera_sched): the wave tiles in dispatch order (null: bottom-up
-  // row order), and per-tile render times to record (s_memrealtime ticks), or null
+  // camera launches of one frame (rtx_render_camera_sched): the dispatch units (the persistent
+  // launch's wave tiles, else the grid's block tiles) in dispatch order (null: bottom-up row order),
+  // and per-unit render times to record (s_memrealtime ticks), or null
   const uint32_t* tile_order;
   uint32_t* tile_cost;
 };
@@ -596,21 +597,6 @@ __device__ __forceinline__ void nearest_range(const cdouble* cg, int first, int 
   }
 }
 
-// The culling tree's node array for the wave's rays: the nearest-first layout of the wave's majority
-// direction octant when the packer stored all eight (RTX_H_NODEOCT), else the single layout. Any
-// layout visits the same nodes under the same test; nearest-first finds near hits early, so the far
-// subtrees fail their node test against the shorter t_nearest (or, for shadow rays, an occluder ends
-// the walk sooner).
-__device__ __forceinline__ const cdouble* tree_nodes(const cdouble* sc, double dx, double dy, double dz) {
-  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
-  if (sc[RTX_H_NODEOCT] == 0.0) return nodes;
-  const int n = __builtin_popcountll(__ballot(1));
-  const int o = (2 * __builtin_popcountll(__ballot(dx < 0.0)) > n ? 1 : 0) |
-                (2 * __builtin_popcountll(__ballot(dy < 0.0)) > n ? 2 : 0) |
-                (2 * __builtin_popcountll(__ballot(dz < 0.0)) > n ? 4 : 0);
-  return nodes + o * (int)sc[RTX_H_NNODES] * RTX_NODE_WORDS;
-}
-
 // Nearest hit through the culling tree: the always-tested spheres, then a stackless depth-first
 // walk that enters a node when any lane of the wave may hit it before its current nearest t.
 // Evaluation order differs from scene order, which the result does not depend on: the nearest t
@@ -619,7 +605,7 @@ template <bool CAM, typename Wk>
 __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double oy, double oz, double dx, double dy,
                                             double dz, double& tmin, int& hit, bool& tie, double tame, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
-  const cdouble* nodes = tree_nodes(sc, dx, dy, dz);
+  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
   const double oo = dot3(ox, oy, oz, ox, oy, oz);
   tmin = FARAWAY;
@@ -694,7 +680,7 @@ template <typename Wk>
 __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy, double qz, double qq, double lx,
                                         double ly, double lz, double tself, int hs, double tame, Wk& wk) {
   const cdouble* cg = sc + (int)sc[RTX_H_CGEO];
-  const cdouble* nodes = tree_nodes(sc, lx, ly, lz);
+  const cdouble* nodes = sc + (int)sc[RTX_H_NODES];
   const int nn = (int)sc[RTX_H_NNODES];
   const int nal = (int)sc[RTX_H_NALWAYS];
   bool lit = true;
@@ -1898,6 +1884,7 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
   // -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%)
   constexpr bool BEAM = TP >= 2 && !DEEP;
   extern __shared__ double lds_tab[];
+  const uint64_t t_entry = p0.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;  // (learning the dispatch order)
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
     // a blob that is not a packed scene of p.nsph spheres (the LDS table and every sphere loop are
@@ -1968,8 +1955,18 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
   // one tile per block. Bottom tile rows are dispatched first: they hold the ground and the
   // spheres, whose pixels run long bounce chains, while sky rows finish at level 0 and so fill the
   // end of the grid (longest-first order; A/B: C2 -10%, C5 -8%, C4 -2%). Output does not depend on
-  // the order.
-  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, blockIdx.x, gridDim.y - 1 - blockIdx.y, true, lds_tab);
+  // the order. Blocks are dispatched in blockIdx order: a host order (camera launches,
+  // rtx_render_camera_sched) maps dispatch slot b to block tile order[b], block tile t being
+  // (t % gridDim.x, bottom-up row t / gridDim.x), and a cost record takes each block's time.
+  int bx = blockIdx.x, by = gridDim.y - 1 - blockIdx.y, tb = blockIdx.y * gridDim.x + blockIdx.x;
+  if (p.tile_order) {
+    tb = (int)((const uint32_t __attribute__((address_space(4)))*)p.tile_order)[tb];
+    bx = tb % gridDim.x;
+    by = gridDim.y - 1 - tb / gridDim.x;
+  }
+  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, bx, by, true, lds_tab);
+  if (p.tile_cost && (threadIdx.x & 63) == 0)  // the block's time: the slowest of its waves
+    atomicMax(p.tile_cost + tb, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_entry));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2413,6 +2410,17 @@ WsLayout ws_layout(int64_t n, int max_bounces) {
 
 size_t ws_bytes(int64_t n, int max_bounces) { return ws_layout(n, max_bounces).total; }
 
+// The block-tile grid of a camera launch that is not persistent: the TREE = false kernels (scenes below
+// kTreeMinSpheres, launch_fast_lds_s) use wave_w<false>() pixels per wave row.
+void block_grid(int nsph, int width, int n_rows, int64_t& gx, int64_t& gy) {
+  const bool small = nsph < kTreeMinSpheres;
+  const int wx = small ? waves_x<false>() : waves_x<true>();
+  const int tw = wx * (small ? wave_w<false>() : wave_w<true>());
+  const int th = (kFastWaves / wx) * (64 / (small ? wave_w<false>() : wave_w<true>()));
+  gx = (width + tw - 1) / tw;
+  gy = (n_rows + th - 1) / th;
+}
+
 // Persistent launch (p.n_fetch > 0 on entry): as many blocks as the device holds at once, at most one
 // wave per tile; sets n_fetch to the counters in use (every counter needs at least one wave).
 template <typename K>
@@ -2547,14 +2555,8 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
     dim3 grid;
-    // block tiles: the TREE = false kernels (scenes below kTreeMinSpheres, launch_fast_lds_s) use
-    // wave_w<false>() pixels per wave row
-    const bool small = p.nsph < kTreeMinSpheres;
-    const int wx = small ? waves_x<false>() : waves_x<true>();
-    const int tw = wx * (small ? wave_w<false>() : wave_w<true>());
-    const int th = (kFastWaves / wx) * (64 / (small ? wave_w<false>() : wave_w<true>()));
-    const int tx = p.mode == 0 ? (p.width + tw - 1) / tw : (int)((p.n + kFastBlock - 1) / kFastBlock);
-    const int ty = p.mode == 0 ? (p.n_rows + th - 1) / th : 1;
+    int64_t tx = (p.n + kFastBlock - 1) / kFastBlock, ty = 1;
+    if (p.mode == 0) block_grid(p.nsph, p.width, p.n_rows, tx, ty);
     p.n_fetch = 0;
     if (p.nsph >= kPersistMinSpheres && p.mode == 0 && p.n_frames == 1) {
       p.n_tiles_x = (p.width + kWaveW - 1) / kWaveW;  // wave tiles
@@ -2680,11 +2682,17 @@ size_t rtx_workspace_bytes(int64_t n_rays, int max_bounces) {
   return ws_bytes(n_rays, max_bounces);
 }
 
-int rtx_wave_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles) {
+int rtx_sched_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles) {
   if (!n_tiles) return fail(RTX_E_ARG, "null pointer argument%s", "");
-  *n_tiles = n_spheres >= kPersistMinSpheres && width > 0 && n_local_rows > 0
-                 ? (int64_t)((width + kWaveW - 1) / kWaveW) * ((n_local_rows + kWaveH - 1) / kWaveH)
-                 : 0;
+  *n_tiles = 0;
+  if (width <= 0 || n_local_rows <= 0 || n_spheres <= 0) return RTX_OK;
+  if (n_spheres >= kPersistMinSpheres) {  // persistent launch: wave tiles
+    *n_tiles = (int64_t)((width + kWaveW - 1) / kWaveW) * ((n_local_rows + kWaveH - 1) / kWaveH);
+    return RTX_OK;
+  }
+  int64_t gx, gy;  // one block tile per block (run_render's grid)
+  block_grid(n_spheres, width, n_local_rows, gx, gy);
+  *n_tiles = gx * gy;
   return RTX_OK;
 }
 
@@ -2721,7 +2729,7 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
   p.out_kind = out_kind;
   p.stats = (unsigned long long*)stats;
   p.deferred_out = deferred_out;
-  p.tile_order = tile_order;  // used by the persistent launch only (rtx_wave_tiles > 0)
+  p.tile_order = tile_order;  // rtx_sched_tiles units of this launch (the first pass: mode 0, one frame)
   p.tile_cost = tile_cost;
   return run_render(p, workspace, workspace_bytes, (hipStream_t)stream, (flags & RTX_F_NO_GENERAL) != 0);
 }

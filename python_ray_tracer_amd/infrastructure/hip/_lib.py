@@ -49,7 +49,7 @@ H_MAGIC, H_NSPH, H_CAM, H_LIGHT, H_DOMEC, H_NDOME, H_DOMEI = 0, 1, 2, 5, 8, 11, 
 H_XSTART, H_XSTEP, H_XSTOP, H_XFIX = 20, 21, 22, 23
 H_YSTART, H_YSTEP, H_YSTOP, H_YFIX = 24, 25, 26, 27
 H_VZ, H_VZ2, H_W, H_H, H_CAMOO = 28, 29, 30, 31, 32
-H_NNODES, H_NALWAYS, H_NODES, H_CGEO, H_TAME, H_MAT0, H_SHGRID, H_SINRED, H_NODEOCT = 33, 34, 35, 36, 37, 38, 39, 40, 41
+H_NNODES, H_NALWAYS, H_NODES, H_CGEO, H_TAME, H_MAT0, H_SHGRID, H_SINRED = 33, 34, 35, 36, 37, 38, 39, 40
 SIN_TFT_MAX = 2.0 ** 20 / (10.0 * 3.141592653589793 * 1.001)  # thin-film thickness bound of RTX_H_SINRED
 SHGRID_WORDS = 13
 TAME_BOUND = 2.0 ** 60
@@ -57,7 +57,7 @@ TAME_BOUND = 2.0 ** 60
 G_CX, G_CY, G_CZ, G_CC, G_RR, G_INVR, G_C0, G_IDX = 0, 1, 2, 3, 4, 5, 6, 7
 # culling-tree node words
 NODE_WORDS = 12
-N_LOX, N_LOY, N_LOZ, N_HIX, N_HIY, N_HIZ, N_FIRST, N_COUNT, N_SKIP, N_MARGIN, N_AXIS = range(11)
+N_LOX, N_LOY, N_LOZ, N_HIX, N_HIY, N_HIZ, N_FIRST, N_COUNT, N_SKIP, N_MARGIN = range(10)
 # material words
 (M_G, M_DG, M_TEX, M_TR, M_TG, M_TB, M_A2, M_A2M1, M_1MA2, M_F0, M_1MF0, M_IG, M_TFW, M_TFT, M_HS, M_1MHS,
  M_ROUGH, M_REFL, M_IOR, M_TFIOR) = range(20)
@@ -82,7 +82,7 @@ EXPORTS = (
     "rtx_selftest_math",
     "rtx_assemble_rows",
     "rtx_shade_hits",
-    "rtx_wave_tiles",
+    "rtx_sched_tiles",
     "rtx_render_camera_sched",
     "rtx_rccl_load",
     "rtx_comm_unique_id",
@@ -133,7 +133,7 @@ _SIGS = {
                                 ctypes.POINTER(_c_void_p), _i64, ctypes.c_uint, ctypes.POINTER(_c_void_p)]),
     "rtx_tiles_submit": (_i32, [_c_void_p, _i32, _c_void_p, _i32, _i32, _c_void_p, _size, ctypes.c_uint, _c_void_p,
                                 _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
-    "rtx_wave_tiles": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "rtx_sched_tiles": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "rtx_render_camera_sched": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
                                        _c_void_p, _size, _c_void_p, _c_void_p, ctypes.c_uint, _c_void_p, _c_void_p,
                                        _c_void_p]),

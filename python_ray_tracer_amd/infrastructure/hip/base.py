@@ -227,7 +227,7 @@ class HipRenderer(Renderer):
         self._scene_cache: dict = {}
         # capped camera renders known to defer no ray (or probing): see _general_plan
         self._defers: dict = {}
-        # persistent launches: the wave-tile dispatch order learnt per (scene, tile, cap), see _sched_plan
+        # camera launches: the dispatch order learnt per (scene, tile, cap), see _sched_plan
         self.learn_tile_order = bool(learn_tile_order)
         self._sched: dict = {}
         self._ws = None
@@ -378,7 +378,7 @@ class HipRenderer(Renderer):
         """What a camera launch of one row tile needs: (blob, n_spheres, local rows, workspace, flags,
         probe, key, tile order, tile cost) — the scene's device blob (cached by content, or the
         caller's, checked), the general-kernel plan of a capped render (_general_plan) and the
-        persistent launch's dispatch order (_sched_plan)."""
+        launch's dispatch order (_sched_plan)."""
         H = int(scene.camera.height)
         key = None
         if blob is None:
@@ -399,12 +399,12 @@ class HipRenderer(Renderer):
         return blob, n_spheres, rows, ws, flags, probe, key, order, cost
 
     def _sched_plan(self, key, width, rows, n_spheres):
-        """(tile_order, tile_cost) of a persistent launch (rtx_render_camera_sched; scenes of >= 32
-        spheres). A few wave tiles with long reflection chains can run alone at the end of the
-        launch; handing the longest tiles out first removes that drain. The render is deterministic
+        """(tile_order, tile_cost) of a camera launch (rtx_render_camera_sched). The launch hands
+        out its units (wave tiles of a persistent launch, block tiles otherwise) bottom-up; a few
+        units with long reflection chains can then run alone at its end. The render is deterministic
         (same blob content, tile and cap: the same rays), so the first launch of a key records every
-        tile's render time (tile_cost, copied to pinned memory behind an event, nothing waits) and,
-        once it has landed, later launches of the key pass the tiles in descending cost order. Output
+        unit's render time (tile_cost, copied to pinned memory behind an event; nothing waits) and,
+        once that has landed, later launches of the key hand the units out longest first. Output
         does not depend on the order."""
         st = self._sched.get(key)
         if st is not None and st[0] == "order":
@@ -419,9 +419,9 @@ class HipRenderer(Renderer):
             self._sched[key] = ("order", dev)
             return dev, None
         nt = ctypes.c_int64()
-        L.check(self._lib.rtx_wave_tiles(width, rows, n_spheres, ctypes.byref(nt)), "rtx_wave_tiles")
-        if nt.value <= 0:
-            self._sched[key] = ("order", None)  # not a persistent launch: nothing to order
+        L.check(self._lib.rtx_sched_tiles(width, rows, n_spheres, ctypes.byref(nt)), "rtx_sched_tiles")
+        if nt.value <= 1:
+            self._sched[key] = ("order", None)  # nothing to order
             return None, None
         if len(self._sched) >= 64:
             self._sched.pop(next(iter(self._sched)))

@@ -327,13 +327,6 @@ def _sah_split(idx, centers, radii):
     return best[1], best[2]
 
 
-# The tree is stored once per ray-direction octant (RTX_H_NODEOCT): layout o visits every inner
-# node's children nearest-first for directions of that octant, so a nearest-hit walk finds near hits
-# early and the far subtrees fail the node test against the shorter t_nearest. The kernel picks the
-# layout of the wave's majority octant; the leaves' sphere ranges are shared.
-BVH_OCTANT_LAYOUTS = True
-
-
 def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarray:
     centers = geo[:, L.G_CX:L.G_CZ + 1]
     radii = np.sqrt(geo[:, L.G_RR])
@@ -341,13 +334,10 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
     small = [i for i in range(S) if i not in set(huge)]
     order = list(huge)
     nodes = []
-    tree = []  # (node record, split axis or -1, children) in build order: the octant layouts' source
 
     def rec(idx):
         me = len(nodes)
         nodes.append(None)
-        entry = [None, -1, []]
-        tree.append(entry)
         lo, hi = _box(centers[idx], radii[idx])
         c = (lo + hi) * 0.5
         R = float(np.sqrt(((hi - lo) ** 2).sum())) * 0.5
@@ -365,66 +355,30 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
                 ar = _area(*_box(centers[right], radii[right]))
                 if a > 0 and 2 * BVH_NODE_COST + (al * len(left) + ar * len(right)) / a < len(idx):
                     split = (left, right)
-        entry[0] = node
         if split is None:
             node[L.N_FIRST] = len(order)
             node[L.N_COUNT] = len(idx)
             order.extend(sorted(idx))
         else:
             nodes[me] = node
-            # the split axis: the one along which the two children's centres differ most
-            cl = centers[split[0]].mean(axis=0)
-            cr = centers[split[1]].mean(axis=0)
-            entry[1] = int(np.argmax(np.abs(cr - cl)))
-            node[L.N_AXIS] = float(entry[1])
-            kl = len(tree)
             rec(split[0])
-            kr = len(tree)
             rec(split[1])
-            entry[2] = [kl, kr] if cl[entry[1]] <= cr[entry[1]] else [kr, kl]  # (low side, high side)
         node[L.N_SKIP] = len(nodes)
         nodes[me] = node
 
     if small:
         rec(small)
     node_arr = np.asarray(nodes, dtype=np.float64).reshape(-1, L.NODE_WORDS)
-    octant = BVH_OCTANT_LAYOUTS and len(nodes) > 1
-    if octant:
-        layouts = [_layout(tree, o) for o in range(8)]
-        node_arr = np.concatenate(layouts)
     cgeo = geo[order].copy()
     cgeo[:, L.G_IDX] = order
     hdr_nodes = blob.size
     hdr_cgeo = hdr_nodes + node_arr.size
     out = np.concatenate([blob, node_arr.ravel(), cgeo.ravel()])
     out[L.H_NNODES] = len(nodes)
-    out[L.H_NODEOCT] = 1.0 if octant else 0.0
     out[L.H_NALWAYS] = len(huge)
     out[L.H_NODES] = hdr_nodes
     out[L.H_CGEO] = hdr_cgeo
     return out
-
-
-def _layout(tree, octant: int) -> np.ndarray:
-    """Depth-first node array of the tree for direction octant ``octant`` (bit a set: component a
-    negative): at each inner node the child on the ray's near side of the split comes first (the
-    low-side child for a positive component). Skip links follow the layout."""
-    out = []
-
-    def emit(k):
-        node, axis, kids = tree[k]
-        me = len(out)
-        out.append(list(node))
-        if axis >= 0:
-            a, b = kids
-            if (octant >> axis) & 1:
-                a, b = b, a
-            emit(a)
-            emit(b)
-        out[me][L.N_SKIP] = len(out)
-
-    emit(0)
-    return np.asarray(out, dtype=np.float64).reshape(-1, L.NODE_WORDS)
 
 
 # --- shadow grid -----------------------------------------------------------------------------

@@ -1,9 +1,10 @@
-"""Longest-first dispatch of the persistent launch (rtx_render_camera_sched, HipRenderer._sched_plan).
+"""Longest-first dispatch of camera launches (rtx_render_camera_sched, HipRenderer._sched_plan).
 
-A scene of >= 32 spheres renders as persistent waves fetching 8x8 wave tiles. HipRenderer records
-every tile's render time on the first launch of a (scene, tile, cap) and hands the tiles out
-longest first from then on. The order changes when a tile is rendered, never what it renders: the
-frames must equal those of a renderer that keeps the bottom-up order, bit for bit, and the oracle.
+A scene of >= 32 spheres renders as persistent waves fetching 8x8 wave tiles, smaller scenes as one
+block tile per block. HipRenderer records every unit's render time on the first launch of a
+(scene, tile, cap) and hands the units out longest first from then on. The order changes when a
+unit is rendered, never what it renders: the frames must equal those of a renderer that keeps the
+bottom-up order, bit for bit, and the oracle.
 """
 
 import numpy as np
@@ -20,14 +21,23 @@ def _dev():
 
 
 def test_learnt_order_leaves_frames_unchanged():
+    """Persistent (40 spheres), small (README, TREE = false) and culled one-block-per-tile (16
+    spheres) launches, capped and unbounded, whole frames and row tiles."""
     dev = _dev()
+    from python_ray_tracer_amd import scenes
+
+    for spec, Bs in ((scenes.random_spec(40, 7, 200, 131), (3, 5, None)), (scenes.readme_spec(203, 117), (3, None)),
+                     (scenes.random_spec(16, 2, 150, 97), (4,))):
+        _check(spec, Bs, dev)
+
+
+def _check(spec, Bs, dev):
     from oracle import numpy_oracle as O
     from python_ray_tracer_amd import scenes
     from python_ray_tracer_amd.infrastructure.hip import HipRenderer
 
-    spec = scenes.random_spec(40, 7, 200, 131)
     scene = scenes.build_scene(spec)
-    for B in (3, 5, None):
+    for B in Bs:
         plain = HipRenderer(max_bounces=B, color_dtype=torch.float64, device=dev, learn_tile_order=False)
         learn = HipRenderer(max_bounces=B, color_dtype=torch.float64, device=dev)
         want = plain.render_tile(scene)
@@ -40,12 +50,12 @@ def test_learnt_order_leaves_frames_unchanged():
             assert "order" in states, states
             for g in got:
                 assert torch.equal(g, ref), (B, rb, parts, part)
-        # the learnt order is a permutation of the wave tiles
+        # the learnt order is a permutation of the launch's units
         for st in learn._sched.values():
             if st[0] == "order" and st[1] is not None:
                 o = st[1].cpu().numpy()
                 assert np.array_equal(np.sort(o), np.arange(len(o)))
-        if B == 3:
-            ora = O.render(O.scene_from_spec(spec), 3)
+        if B == Bs[0]:
+            ora = O.render(O.scene_from_spec(spec), B)
             assert float(np.abs(learn.render_tile(scene).cpu().numpy() - ora).max()) <= 1e-12
             assert torch.equal(learn.render_tile(scene), want)
