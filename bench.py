@@ -79,6 +79,10 @@ def parse():
     ap.add_argument("--no-tile-order", action="store_true",
                     help="camera launches keep the bottom-up tile order instead of the longest-first order "
                          "HipRenderer learns from its first launch of a scene (A/B)")
+    ap.add_argument("--loopback", action="store_true",
+                    help="tiles mode on one GPU: a one-rank RCCL group whose plan still sends its tile through "
+                         "RCCL (to itself) and assembles it, two frames in flight: how the gather's RCCL kernels "
+                         "share the GPU with the next frame's render")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -150,7 +154,11 @@ def main():
         # strong scaling: every rank renders its interleaved row tile of ONE frame into a gather
         # buffer, one gather to rank 0, one device un-permute there; two slots, so the gather of
         # frame k overlaps the render of frame k+1 (python_ray_tracer_amd/distributed.py)
-        step, drain = tiles_stepper(r, scene, world, args.row_block, "u8" if args.out == "u8" else None)
+        if args.loopback and world == 1 and not dist.is_initialized():
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                    device_id=dev)
+        step, drain = tiles_stepper(r, scene, world, args.row_block, "u8" if args.out == "u8" else None,
+                                    loopback=args.loopback)
         px_per_step = W * H
 
     def barrier():  # every rank's queued GPU work done, then all ranks meet
@@ -346,7 +354,7 @@ def main():
         dist.destroy_process_group()
 
 
-def tiles_stepper(r, scene, world, row_block, out):
+def tiles_stepper(r, scene, world, row_block, out, loopback=False):
     """(step, drain) of the strong-scaling tiles mode: TileGather with two slots; step k submits
     frame k and finishes frame k-1 (its gather overlapped frame k's render); drain finishes the last
     one. Without a process group: the whole frame rendered into a pre-allocated buffer."""
@@ -364,7 +372,7 @@ def tiles_stepper(r, scene, world, row_block, out):
     from python_ray_tracer_amd.distributed import TileGather
 
     tg = TileGather(r, int(scene.camera.width), int(scene.camera.height), row_block=row_block, out=out, slots=2,
-                    persistent_frames=True)
+                    persistent_frames=True, loopback=loopback)
     state = {"k": 0, "open": None}
 
     def step():

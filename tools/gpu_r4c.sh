@@ -23,3 +23,6 @@ run C4_order 200 python bench.py --config C4 --steps 30 --warmup 3 $B --json-out
 run C4_plain 200 python bench.py --config C4 --steps 30 --warmup 3 $B --no-tile-order --json-out $O/C4_plain.json
 run emul_C4 300 python bench.py --config C4 --emulate-parts 2,4,8 --steps 20 --json-out $O/emul_C4.json
 run emul_C2 300 python bench.py --config C2 --emulate-parts 2,4,8 --steps 50 --json-out $O/emul_C2.json
+run C4_tiles_direct 200 python bench.py --config C4 --mode tiles --steps 10 --warmup 2 --cpu-seconds 0 --json-out $O/C4_tiles_direct.json
+run C4_tiles_loop 200 python bench.py --config C4 --mode tiles --loopback --steps 10 --warmup 2 --cpu-seconds 0 --json-out $O/C4_tiles_loop.json
+run C2_tiles_loop 200 python bench.py --config C2 --mode tiles --loopback --steps 200 --warmup 20 --cpu-seconds 0 --json-out $O/C2_tiles_loop.json
