@@ -251,6 +251,12 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
  *    flag (the workspace counters stay clean, so later calls are unaffected). Uncapped renders
  *    ignore it. */
 #define RTX_F_NO_GENERAL 1u
+/* RTX_F_RESERVE(n): a persistent launch (>= 32 spheres, one frame) sizes its grid n blocks below what
+ * the device holds at once, leaving room for the kernels of a collective running beside it (the
+ * row-tiled frame's RCCL gather of the previous frame: the persistent waves would otherwise hold
+ * every slot until they finish). n < 4096. */
+#define RTX_F_RESERVE_SHIFT 4
+#define RTX_F_RESERVE(n) ((((unsigned)(n)) & 0xFFFu) << RTX_F_RESERVE_SHIFT)
 int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int height,
                          int row_block, int n_parts, int part, int n_local_rows,
                          int max_bounces, void* out, int out_kind,
@@ -350,7 +356,9 @@ int rtx_comm_unique_id(void* id_out);
 int rtx_comm_init(const void* id, int world, int rank, void** comm_out);
 int rtx_comm_destroy(void* comm);
 /* rtx_tiles_create flags. RTX_TILES_LOOPBACK: a one-rank plan whose tile still travels through
- * RCCL (sent to and received from itself, then assembled): the gather path on a single GPU. */
+ * RCCL (sent to and received from itself, then assembled): the gather path on a single GPU.
+ * RTX_F_RESERVE(n): every render of a plan that gathers (world > 1 or loopback) passes it, so that
+ * frame k's RCCL kernels find free slots beside frame k+1's persistent render. */
 #define RTX_TILES_LOOPBACK 1u
 /* A plan for frames of width x height in row blocks of row_block, out_kind RTX_OUT_*, `slots`
  * frames in flight (<= RTX_TILES_MAX_SLOTS). Per slot s, caller-owned device buffers kept for the

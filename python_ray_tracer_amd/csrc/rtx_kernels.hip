@@ -182,6 +182,7 @@ struct Params {
   // and per-unit render times to record (s_memrealtime ticks), or null
   const uint32_t* tile_order;
   uint32_t* tile_cost;
+  int reserve;  // RTX_F_RESERVE: block slots the persistent launch leaves free (host side only)
 };
 
 // Deferred-list entry (uint64): pixel | frame << 40 | (rays counted through level a) + 1 << 56 |
@@ -2429,7 +2430,8 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kFastBlock, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
   const int64_t nt = (int64_t)p.n_tiles_x * p.n_tiles_y;
-  int64_t blocks = (int64_t)per_cu * device_cus();
+  int64_t blocks = (int64_t)per_cu * device_cus() - p.reserve;  // (room for a concurrent collective)
+  if (blocks < 8) blocks = 8;
   const int64_t need = (nt + kFastWaves - 1) / kFastWaves;
   if (blocks > need) blocks = need;
   if (blocks >= 8) blocks -= blocks % 8;  // whole XCD groups (the kernel numbers waves XCD-major)
@@ -2712,7 +2714,8 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
   if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
       n_local_rows < 0 || n_local_rows > height)
     return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
-  if (flags & ~(unsigned)RTX_F_NO_GENERAL) return fail(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
+  if (flags & ~(unsigned)(RTX_F_NO_GENERAL | RTX_F_RESERVE(0xFFF)))
+    return fail(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
   Params p{};
   p.scene = scene;
   p.nsph = n_spheres;
@@ -2731,6 +2734,7 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
   p.deferred_out = deferred_out;
   p.tile_order = tile_order;  // rtx_sched_tiles units of this launch (the first pass: mode 0, one frame)
   p.tile_cost = tile_cost;
+  p.reserve = (int)((flags >> RTX_F_RESERVE_SHIFT) & 0xFFFu);
   return run_render(p, workspace, workspace_bytes, (hipStream_t)stream, (flags & RTX_F_NO_GENERAL) != 0);
 }
 

@@ -76,6 +76,7 @@ struct Tiles {
   int local_rows;
   int device;
   bool loop;  // RTX_TILES_LOOPBACK: a one-rank plan whose tile still goes through RCCL (send to itself)
+  unsigned reserve;  // RTX_F_RESERVE bits passed to every render (plans that gather)
   hipStream_t cs;  // collective + assembly stream
   void* send[RTX_TILES_MAX_SLOTS];
   void* recv[RTX_TILES_MAX_SLOTS];
@@ -157,7 +158,8 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   if (width <= 0 || height <= 0 || row_block <= 0) return err(RTX_E_ARG, "bad frame/tile geometry%s", "");
   if (out_kind < 0 || out_kind > 2) return err(RTX_E_ARG, "bad out_kind%s %lld", "", out_kind);
   if (slots < 1 || slots > RTX_TILES_MAX_SLOTS) return err(RTX_E_ARG, "bad slot count%s (%lld)", "", slots);
-  if (flags & ~(unsigned)RTX_TILES_LOOPBACK) return err(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
+  if (flags & ~(unsigned)(RTX_TILES_LOOPBACK | RTX_F_RESERVE(0xFFF)))
+    return err(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
   const bool loop = world == 1 && (flags & RTX_TILES_LOOPBACK);
   if ((world > 1 || loop) && (!comm || !rccl_ready()))
     return err(RTX_E_COMM, "world > 1 (or a loopback plan) needs an RCCL communicator%s", "");
@@ -183,6 +185,7 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   t->part_bytes = part_bytes;
   t->local_rows = local_rows(height, row_block, world, rank);
   t->loop = loop;
+  t->reserve = (world > 1 || loop) ? (flags & RTX_F_RESERVE(0xFFF)) : 0u;
   (void)hipGetDevice(&t->device);
   hipError_t e = hipStreamCreateWithFlags(&t->cs, hipStreamNonBlocking);
   for (int s = 0; s < slots && e == hipSuccess; ++s) {
@@ -224,7 +227,7 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
                               : t->send[slot];
   if (int rc = rtx_render_camera_sched(scene, n_spheres, t->width, t->height, t->row_block, t->world, t->rank,
                                        t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes,
-                                       nullptr, stream, flags, deferred_out, tile_order, tile_cost))
+                                       nullptr, stream, flags | t->reserve, deferred_out, tile_order, tile_cost))
     return rc;
   if (direct) return RTX_OK;
   hipError_t e = hipEventRecord(t->rendered[slot], s);

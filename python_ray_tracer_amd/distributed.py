@@ -32,6 +32,12 @@ import torch
 from python_ray_tracer_amd import tiling
 
 
+# Block slots a gathering plan's persistent renders leave free for the previous frame's RCCL kernels
+# (RTX_F_RESERVE): without them the gather waits for the render to end (one GPU, C4 loopback: 2,253
+# against 2,062 us per step).
+COMM_RESERVE_BLOCKS = 0
+
+
 # RCCL communicators of the native path, one per (process group, rank, device): creating one costs
 # a rendezvous, so TileGathers of the same group share it for the life of the process
 _COMMS: dict = {}
@@ -70,13 +76,15 @@ def rccl_comm(group, root: int, device):
 class TileGather:
     def __init__(self, renderer, width: int, height: int, *, group=None, row_block: int = 8, dst: int = 0,
                  out: str | None = None, slots: int = 2, native: bool | None = None,
-                 persistent_frames: bool = False, loopback: bool = False) -> None:
+                 persistent_frames: bool = False, loopback: bool = False, comm_reserve: int | None = None) -> None:
         """``native``: drive each frame through rtx_tiles_submit (default: under RCCL with a
         renderer that has ``submit_tiles``); False keeps torch.distributed.gather. ``persistent_frames``
         (native root): assemble every frame of a slot into one buffer kept by the slot, so a frame
         returned by finish(slot) is overwritten by that slot's next frame (the bench); otherwise each
         frame gets a new tensor. ``loopback`` (native, one rank): the tile still travels through RCCL
-        (sent to and received from the rank itself), the gather path on one GPU (tests)."""
+        (sent to and received from the rank itself), the gather path on one GPU (tests).
+        ``comm_reserve``: block slots every persistent render of a gathering plan leaves free for the
+        previous frame's RCCL kernels (RTX_F_RESERVE; default COMM_RESERVE_BLOCKS)."""
         import torch.distributed as dist
 
         self._dist = dist
@@ -100,7 +108,8 @@ class TileGather:
         if native is None:
             native = not self.gloo and hasattr(renderer, "submit_tiles")
         if native:
-            self._init_native(dtype, plen, slots, persistent_frames, loopback and self.world == 1)
+            self._init_native(dtype, plen, slots, persistent_frames, loopback and self.world == 1,
+                              COMM_RESERVE_BLOCKS if comm_reserve is None else int(comm_reserve))
             return
         # zero-filled once: the padding beyond a short part's tile is sent but never read
         self.send = [torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]
@@ -111,7 +120,7 @@ class TileGather:
         self._recv_lists = [list(b.unbind(0)) for b in self.recv] if self.recv is not None else None
         self._views = [b[:self.n].view(self.shape) for b in self.send]
 
-    def _init_native(self, dtype, plen, slots, persistent_frames, loop) -> None:
+    def _init_native(self, dtype, plen, slots, persistent_frames, loop, reserve) -> None:
         import ctypes
 
         from python_ray_tracer_amd.infrastructure.hip import _lib as L
@@ -138,7 +147,8 @@ class TileGather:
         with torch.cuda.device(self.device):
             L.check(self._lib.rtx_tiles_create(comm, self.world, self.rank, self.dst, self.W, self.H, self.rb, kind,
                                                slots, send, recv, plen * torch.empty((), dtype=dtype).element_size(),
-                                               L.TILES_LOOPBACK if loop else 0, ctypes.byref(plan)),
+                                               (L.TILES_LOOPBACK if loop else 0) | ((reserve & 0xFFF) << L.F_RESERVE_SHIFT),
+                                               ctypes.byref(plan)),
                     "rtx_tiles_create")
         self.plan = plan.value
 
