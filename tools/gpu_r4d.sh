@@ -12,3 +12,11 @@ for r in 0 16 64 128 256; do
 done
 run direct2 200 python bench.py $T --json-out $O/direct2.json
 run loop_C2 200 python bench.py --config C2 --mode tiles --steps 200 --warmup 20 --cpu-seconds 0 --loopback --json-out $O/loop_C2.json
+# C4 kernel variants (tools/ab_build.py --only-b 5; bench through RTX_HIP_LIB, learnt order on)
+for v in base5 nopersist nobeam base5; do
+  RTX_HIP_LIB=ab/$v.so run C4_$v 200 python bench.py --config C4 --steps 30 --warmup 3 --cpu-seconds 0 --no-secondary --json-out $O/C4_$v.json
+done
+for i in 1 2; do
+  run C2main_order_$i 120 python bench.py --config C2main --steps 400 --warmup 20 --cpu-seconds 0 --no-secondary --json-out $O/C2main_order_$i.json
+  run C2main_plain_$i 120 python bench.py --config C2main --steps 400 --warmup 20 --cpu-seconds 0 --no-secondary --no-tile-order --json-out $O/C2main_plain_$i.json
+done
