@@ -352,8 +352,9 @@ int rtx_rccl_load(const char* path);
 /* ncclGetUniqueId into id_out (128 bytes): the root calls it, the host broadcasts the bytes. */
 int rtx_comm_unique_id(void* id_out);
 /* ncclCommInitRank over `world` ranks (collective: every rank calls it with the same id); the
- * communicator is bound to the current device. */
-int rtx_comm_init(const void* id, int world, int rank, void** comm_out);
+ * communicator is bound to the current device. max_ctas > 0: ncclCommInitRankConfig with
+ * maxCTAs = max_ctas, capping the blocks its kernels take from a render running beside them. */
+int rtx_comm_init(const void* id, int world, int rank, int max_ctas, void** comm_out);
 int rtx_comm_destroy(void* comm);
 /* rtx_tiles_create flags. RTX_TILES_LOOPBACK: a one-rank plan whose tile still travels through
  * RCCL (sent to and received from itself, then assembled): the gather path on a single GPU.

@@ -35,6 +35,7 @@ struct Rccl {
   void* lib = nullptr;
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommInitRankConfig) comm_init_rank_config = nullptr;  // optional (max_ctas)
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
@@ -117,6 +118,7 @@ int rtx_rccl_load(const char* path) {
     g_rccl = Rccl{};
     return err(RTX_E_COMM, "RCCL library lacks a required symbol%s", "");
   }
+  sym(g_rccl.comm_init_rank_config, "ncclCommInitRankConfig");
   return RTX_OK;
 }
 
@@ -129,14 +131,23 @@ int rtx_comm_unique_id(void* id_out) {
   return RTX_OK;
 }
 
-int rtx_comm_init(const void* id, int world, int rank, void** comm_out) {
+int rtx_comm_init(const void* id, int world, int rank, int max_ctas, void** comm_out) {
   if (!id || !comm_out) return err(RTX_E_ARG, "null pointer argument%s", "");
   if (world < 1 || rank < 0 || rank >= world) return err(RTX_E_ARG, "bad world/rank%s (%lld)", "", world);
   if (!rccl_ready()) return err(RTX_E_COMM, "RCCL not loaded (rtx_rccl_load)%s", "");
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
   ncclComm_t c = nullptr;
-  if (ncclResult_t r = g_rccl.comm_init_rank(&c, world, uid, rank)) return nccl_err("ncclCommInitRank", r);
+  if (max_ctas > 0) {  // cap the CTAs (blocks) of the communicator's kernels: the gather runs beside a render
+    if (!g_rccl.comm_init_rank_config) return err(RTX_E_COMM, "RCCL lacks ncclCommInitRankConfig%s", "");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = max_ctas;
+    if (ncclResult_t r = g_rccl.comm_init_rank_config(&c, world, uid, rank, &cfg))
+      return nccl_err("ncclCommInitRankConfig", r);
+  } else if (ncclResult_t r = g_rccl.comm_init_rank(&c, world, uid, rank)) {
+    return nccl_err("ncclCommInitRank", r);
+  }
   *comm_out = c;
   return RTX_OK;
 }

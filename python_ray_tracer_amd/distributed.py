@@ -43,9 +43,12 @@ COMM_RESERVE_BLOCKS = 0
 _COMMS: dict = {}
 
 
-def rccl_comm(group, root: int, device):
+def rccl_comm(group, root: int, device, max_ctas: int | None = None):
     """The library's RCCL communicator over ``group`` (rtx_comm_init): the root's ncclUniqueId is
-    broadcast over the group itself. Collective: every rank of the group calls it."""
+    broadcast over the group itself. Collective: every rank of the group calls it. ``max_ctas``
+    (default: env RTX_COMM_MAX_CTAS, else RCCL's own choice) caps the blocks of its kernels."""
+    import os
+
     import ctypes
 
     import torch.distributed as dist
@@ -54,7 +57,9 @@ def rccl_comm(group, root: int, device):
 
     pg = group if group is not None else dist.group.WORLD
     world, rank = dist.get_world_size(pg), dist.get_rank(pg)
-    key = (getattr(pg, "group_name", id(pg)), world, rank, torch.device(device).index)
+    if max_ctas is None:
+        max_ctas = int(os.environ.get("RTX_COMM_MAX_CTAS", "0"))
+    key = (getattr(pg, "group_name", id(pg)), world, rank, torch.device(device).index, int(max_ctas))
     comm = _COMMS.get(key)
     if comm is not None:
         return comm
@@ -68,7 +73,7 @@ def rccl_comm(group, root: int, device):
     uid = (ctypes.c_char * L.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
     c = ctypes.c_void_p()
     with torch.cuda.device(device):
-        L.check(lib.rtx_comm_init(uid, world, rank, ctypes.byref(c)), "rtx_comm_init")
+        L.check(lib.rtx_comm_init(uid, world, rank, int(max_ctas), ctypes.byref(c)), "rtx_comm_init")
     _COMMS[key] = c.value
     return c.value
 

@@ -128,7 +128,7 @@ _SIGS = {
     "rtx_assemble_rows": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "rtx_rccl_load": (_i32, [ctypes.c_char_p]),
     "rtx_comm_unique_id": (_i32, [_c_void_p]),
-    "rtx_comm_init": (_i32, [_c_void_p, _i32, _i32, ctypes.POINTER(_c_void_p)]),
+    "rtx_comm_init": (_i32, [_c_void_p, _i32, _i32, _i32, ctypes.POINTER(_c_void_p)]),
     "rtx_comm_destroy": (_i32, [_c_void_p]),
     "rtx_tiles_create": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_c_void_p),
                                 ctypes.POINTER(_c_void_p), _i64, ctypes.c_uint, ctypes.POINTER(_c_void_p)]),
