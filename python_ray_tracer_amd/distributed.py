@@ -33,9 +33,11 @@ from python_ray_tracer_amd import tiling
 
 
 # Block slots a gathering plan's persistent renders leave free for the previous frame's RCCL kernels
-# (RTX_F_RESERVE): without them the gather waits for the render to end (one GPU, C4 loopback: 2,253
-# against 2,062 us per step).
-COMM_RESERVE_BLOCKS = 0
+# (RTX_F_RESERVE). One GPU, C4 through a loopback plan (the tile sent to itself over RCCL, 100 MB,
+# then assembled) beside the next frame's render: 2,256-2,273 us per step with no reserve, 2,188-2,207
+# with 64 (16: 2,389; 128: 2,309; 256: 2,569), against 2,060 without the gather
+# (profiles/r4d_gather_ab, r4e_gather_ab); capping RCCL's CTAs at 2, 4 or 8 changed nothing.
+COMM_RESERVE_BLOCKS = 64
 
 
 # RCCL communicators of the native path, one per (process group, rank, device): creating one costs

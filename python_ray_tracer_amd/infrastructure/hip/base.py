@@ -403,36 +403,24 @@ class HipRenderer(Renderer):
         out its units (wave tiles of a persistent launch, block tiles otherwise) bottom-up; a few
         units with long reflection chains can then run alone at its end. The render is deterministic
         (same blob content, tile and cap: the same rays), so the first launch of a key records every
-        unit's render time (tile_cost, copied to pinned memory behind an event; nothing waits) and,
-        once that has landed, later launches of the key hand the units out longest first. Output
-        does not depend on the order."""
-        st = self._sched.get(key)
-        if st is not None and st[0] == "order":
-            return st[1], None
+        unit's render time (tile_cost) and the units sorted by descending time (a device argsort
+        enqueued right behind it: nothing waits, nothing crosses to the host) are the dispatch order
+        of every later launch of the key. Output does not depend on the order."""
+        if key in self._sched:  # the learnt order (None: a launch of a single unit)
+            return self._sched[key], None
         if torch.cuda.is_current_stream_capturing():
             return None, None
-        if st is not None:  # ("cost", event, pinned host copy)
-            if not st[1].query():
-                return None, None
-            order = np.argsort(-st[2].numpy().astype(np.int64), kind="stable").astype(np.int32)
-            dev = torch.from_numpy(order).pin_memory().to(self.device, non_blocking=True)
-            self._sched[key] = ("order", dev)
-            return dev, None
         nt = ctypes.c_int64()
         L.check(self._lib.rtx_sched_tiles(width, rows, n_spheres, ctypes.byref(nt)), "rtx_sched_tiles")
         if nt.value <= 1:
-            self._sched[key] = ("order", None)  # nothing to order
+            self._sched[key] = None  # nothing to order
             return None, None
-        if len(self._sched) >= 64:
-            self._sched.pop(next(iter(self._sched)))
         return None, torch.zeros(nt.value, dtype=torch.int32, device=self.device)
 
     def _cost_landed(self, key, cost) -> None:
-        host = torch.empty(cost.shape, dtype=torch.int32, pin_memory=True)
-        host.copy_(cost, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self._sched[key] = ("cost", ev, host)
+        if len(self._sched) >= 64:
+            self._sched.pop(next(iter(self._sched)))
+        self._sched[key] = torch.argsort(cost, descending=True, stable=True).to(torch.int32)
 
     @_on_device
     def submit_tiles(self, plan, slot: int, scene, row_block: int, n_parts: int, part: int, frame) -> None:
