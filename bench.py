@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--comm-reserve", type=int, default=None,
                     help="tiles mode: block slots a gathering plan's persistent renders leave free for the RCCL "
                          "kernels of the previous frame (default distributed.COMM_RESERVE_BLOCKS)")
+    ap.add_argument("--assemble", action="store_true",
+                    help="tiles mode: gather whole tiles and assemble them on the root instead of moving each row "
+                         "block straight into the root's frame (RTX_TILES_ROWS, the uint8 default) (A/B)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -161,7 +164,8 @@ def main():
             dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                                     device_id=dev)
         step, drain = tiles_stepper(r, scene, world, args.row_block, "u8" if args.out == "u8" else None,
-                                    loopback=args.loopback, comm_reserve=args.comm_reserve)
+                                    loopback=args.loopback, comm_reserve=args.comm_reserve,
+                                    rows=False if args.assemble else None)
         px_per_step = W * H
 
     def barrier():  # every rank's queued GPU work done, then all ranks meet
@@ -357,7 +361,7 @@ def main():
         dist.destroy_process_group()
 
 
-def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=None):
+def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=None, rows=None):
     """(step, drain) of the strong-scaling tiles mode: TileGather with two slots; step k submits
     frame k and finishes frame k-1 (its gather overlapped frame k's render); drain finishes the last
     one. Without a process group: the whole frame rendered into a pre-allocated buffer."""
@@ -375,7 +379,7 @@ def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=
     from python_ray_tracer_amd.distributed import TileGather
 
     tg = TileGather(r, int(scene.camera.width), int(scene.camera.height), row_block=row_block, out=out, slots=2,
-                    persistent_frames=True, loopback=loopback, comm_reserve=comm_reserve)
+                    persistent_frames=True, loopback=loopback, comm_reserve=comm_reserve, rows=rows)
     state = {"k": 0, "open": None}
 
     def step():

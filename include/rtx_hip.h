@@ -361,6 +361,11 @@ int rtx_comm_destroy(void* comm);
  * RTX_F_RESERVE(n): every render of a plan that gathers (world > 1 or loopback) passes it, so that
  * frame k's RCCL kernels find free slots beside frame k+1's persistent render. */
 #define RTX_TILES_LOOPBACK 1u
+/* RTX_TILES_ROWS (uint8 frames): every row block travels on its own, straight into its rows of the
+ * root's frame (one ncclSend / ncclRecv per block; the root's own blocks by one strided device
+ * copy), so the root never runs the assembly pass (a read and a write of the whole frame in HBM,
+ * beside its next render). recv[s] then holds the root's own tile only (part_bytes). */
+#define RTX_TILES_ROWS 2u
 /* A plan for frames of width x height in row blocks of row_block, out_kind RTX_OUT_*, `slots`
  * frames in flight (<= RTX_TILES_MAX_SLOTS). Per slot s, caller-owned device buffers kept for the
  * plan's life: a peer's send[s] (part_bytes) and the root's recv[s] (world * part_bytes: part p at

@@ -77,6 +77,7 @@ struct Tiles {
   int local_rows;
   int device;
   bool loop;  // RTX_TILES_LOOPBACK: a one-rank plan whose tile still goes through RCCL (send to itself)
+  bool rows;  // RTX_TILES_ROWS: each row block travels on its own and lands in the frame (no assembly)
   unsigned reserve;  // RTX_F_RESERVE bits passed to every render (plans that gather)
   hipStream_t cs;  // collective + assembly stream
   void* send[RTX_TILES_MAX_SLOTS];
@@ -93,6 +94,56 @@ int local_rows(int height, int row_block, int n_parts, int p) {  // tiling.n_loc
 }
 
 int64_t bytes_per_pixel(int kind) { return kind == RTX_OUT_F32_SOA ? 12 : kind == RTX_OUT_F64_SOA ? 24 : 3; }
+
+// RTX_TILES_ROWS: the gather moves every row block of a part on its own, straight into its rows of
+// the root's frame (a uint8 row block is contiguous there), so the root never assembles: per peer,
+// one ncclSend per block of its tile (local rows in order), and at the root one ncclRecv per block
+// into frame row ((j * P + p) * rb); the root's own blocks are one strided device copy. Sends and
+// receives between a pair match in order. On the plan's stream after the render; records done.
+int gather_rows(Tiles* t, int slot, bool root, uint8_t* frame) {
+  const int P = t->world, rb = t->row_block;
+  const int64_t rowb = (int64_t)t->width * 3;
+  ncclResult_t r = g_rccl.group_start();
+  if (r != ncclSuccess) return nccl_err("ncclGroupStart", r);
+  const bool sender = t->loop || !root;
+  const int dest = t->loop ? 0 : t->root;
+  if (sender) {
+    const int n = local_rows(t->height, rb, P, t->rank);
+    for (int j = 0; j * rb < n && r == ncclSuccess; ++j) {
+      const int rows = n - j * rb < rb ? n - j * rb : rb;
+      r = g_rccl.send((const uint8_t*)t->send[slot] + (int64_t)j * rb * rowb, (size_t)(rows * rowb), ncclUint8, dest,
+                      t->comm, t->cs);
+    }
+  }
+  if (root) {
+    for (int p = 0; p < P && r == ncclSuccess; ++p) {
+      if (p == t->root && !t->loop) continue;
+      const int n = local_rows(t->height, rb, P, p);
+      for (int j = 0; j * rb < n && r == ncclSuccess; ++j) {
+        const int rows = n - j * rb < rb ? n - j * rb : rb;
+        r = g_rccl.recv(frame + (int64_t)(j * P + p) * rb * rowb, (size_t)(rows * rowb), ncclUint8, p, t->comm, t->cs);
+      }
+    }
+  }
+  const ncclResult_t r2 = g_rccl.group_end();
+  if (r != ncclSuccess) return nccl_err(root ? "ncclRecv" : "ncclSend", r);
+  if (r2 != ncclSuccess) return nccl_err("ncclGroupEnd", r2);
+  hipError_t e = hipSuccess;
+  if (root && !t->loop) {  // the root's own blocks: rows (j P + root) rb .. + rb of the frame
+    const int n = t->local_rows, full = n / rb, tail = n % rb;
+    const uint8_t* own = (const uint8_t*)t->recv[slot];
+    uint8_t* dst0 = frame + (int64_t)t->root * rb * rowb;
+    if (full > 0)
+      e = hipMemcpy2DAsync(dst0, (size_t)(P * rb * rowb), own, (size_t)(rb * rowb), (size_t)(rb * rowb), (size_t)full,
+                           hipMemcpyDeviceToDevice, t->cs);
+    if (e == hipSuccess && tail > 0)
+      e = hipMemcpyAsync(dst0 + (int64_t)full * P * rb * rowb, own + (int64_t)full * rb * rowb, (size_t)(tail * rowb),
+                         hipMemcpyDeviceToDevice, t->cs);
+  }
+  if (e == hipSuccess) e = hipEventRecord(t->done[slot], t->cs);
+  if (e != hipSuccess) return err(RTX_E_LAUNCH, "gather_rows: %s", hipGetErrorString(e));
+  return RTX_OK;
+}
 
 }  // namespace
 
@@ -169,9 +220,12 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   if (width <= 0 || height <= 0 || row_block <= 0) return err(RTX_E_ARG, "bad frame/tile geometry%s", "");
   if (out_kind < 0 || out_kind > 2) return err(RTX_E_ARG, "bad out_kind%s %lld", "", out_kind);
   if (slots < 1 || slots > RTX_TILES_MAX_SLOTS) return err(RTX_E_ARG, "bad slot count%s (%lld)", "", slots);
-  if (flags & ~(unsigned)(RTX_TILES_LOOPBACK | RTX_F_RESERVE(0xFFF)))
+  if (flags & ~(unsigned)(RTX_TILES_LOOPBACK | RTX_TILES_ROWS | RTX_F_RESERVE(0xFFF)))
     return err(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
   const bool loop = world == 1 && (flags & RTX_TILES_LOOPBACK);
+  const bool rows = (flags & RTX_TILES_ROWS) && (world > 1 || loop);
+  if (rows && out_kind != RTX_OUT_U8_HWC)
+    return err(RTX_E_ARG, "RTX_TILES_ROWS needs uint8 frames (a row block is contiguous there)%s", "");
   if ((world > 1 || loop) && (!comm || !rccl_ready()))
     return err(RTX_E_COMM, "world > 1 (or a loopback plan) needs an RCCL communicator%s", "");
   const int rows0 = local_rows(height, row_block, world, 0);  // part 0 has the most rows
@@ -196,6 +250,7 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   t->part_bytes = part_bytes;
   t->local_rows = local_rows(height, row_block, world, rank);
   t->loop = loop;
+  t->rows = rows;
   t->reserve = (world > 1 || loop) ? (flags & RTX_F_RESERVE(0xFFF)) : 0u;
   (void)hipGetDevice(&t->device);
   hipError_t e = hipStreamCreateWithFlags(&t->cs, hipStreamNonBlocking);
@@ -224,9 +279,9 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
   if (root && !frame) return err(RTX_E_ARG, "the root needs a frame buffer%s", "");
   // a one-rank plan without loopback renders straight into the caller's frame on the caller's
   // stream: stream order is all the ordering it needs (no event: each costs the stream a barrier)
-  const bool direct = t->world == 1 && !t->loop;
+  const bool single = t->world == 1 && !t->loop;
   // the slot's buffers are free once its previous frame's gather and assembly have run
-  if (t->used[slot] && !direct) {
+  if (t->used[slot] && !single) {
     if (hipError_t e = hipStreamWaitEvent(s, t->done[slot], 0))
       return err(RTX_E_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
@@ -234,16 +289,17 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
   // a single part IS the frame (local rows = global rows): render straight into it
   void* dst = t->loop        ? t->send[slot]
               : t->world == 1 ? frame
-              : root          ? (uint8_t*)t->recv[slot] + (int64_t)t->root * t->part_bytes
+              : root          ? (uint8_t*)t->recv[slot] + (t->rows ? 0 : (int64_t)t->root * t->part_bytes)
                               : t->send[slot];
   if (int rc = rtx_render_camera_sched(scene, n_spheres, t->width, t->height, t->row_block, t->world, t->rank,
                                        t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes,
                                        nullptr, stream, flags | t->reserve, deferred_out, tile_order, tile_cost))
     return rc;
-  if (direct) return RTX_OK;
+  if (single) return RTX_OK;
   hipError_t e = hipEventRecord(t->rendered[slot], s);
   if (e == hipSuccess) e = hipStreamWaitEvent(t->cs, t->rendered[slot], 0);
   if (e != hipSuccess) return err(RTX_E_LAUNCH, "event: %s", hipGetErrorString(e));
+  if (t->rows) return gather_rows(t, slot, root, (uint8_t*)frame);
   if (ncclResult_t r = g_rccl.group_start()) return nccl_err("ncclGroupStart", r);
   ncclResult_t r = ncclSuccess;
   if (t->loop) {

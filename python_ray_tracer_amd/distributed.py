@@ -83,7 +83,8 @@ def rccl_comm(group, root: int, device, max_ctas: int | None = None):
 class TileGather:
     def __init__(self, renderer, width: int, height: int, *, group=None, row_block: int = 8, dst: int = 0,
                  out: str | None = None, slots: int = 2, native: bool | None = None,
-                 persistent_frames: bool = False, loopback: bool = False, comm_reserve: int | None = None) -> None:
+                 persistent_frames: bool = False, loopback: bool = False, comm_reserve: int | None = None,
+                 rows: bool | None = None) -> None:
         """``native``: drive each frame through rtx_tiles_submit (default: under RCCL with a
         renderer that has ``submit_tiles``); False keeps torch.distributed.gather. ``persistent_frames``
         (native root): assemble every frame of a slot into one buffer kept by the slot, so a frame
@@ -91,7 +92,9 @@ class TileGather:
         frame gets a new tensor. ``loopback`` (native, one rank): the tile still travels through RCCL
         (sent to and received from the rank itself), the gather path on one GPU (tests).
         ``comm_reserve``: block slots every persistent render of a gathering plan leaves free for the
-        previous frame's RCCL kernels (RTX_F_RESERVE; default COMM_RESERVE_BLOCKS)."""
+        previous frame's RCCL kernels (RTX_F_RESERVE; default COMM_RESERVE_BLOCKS). ``rows`` (native,
+        uint8 frames; the default there): every row block travels on its own straight into the
+        root's frame (RTX_TILES_ROWS), with no assembly pass on the root."""
         import torch.distributed as dist
 
         self._dist = dist
@@ -116,7 +119,8 @@ class TileGather:
             native = not self.gloo and hasattr(renderer, "submit_tiles")
         if native:
             self._init_native(dtype, plen, slots, persistent_frames, loopback and self.world == 1,
-                              COMM_RESERVE_BLOCKS if comm_reserve is None else int(comm_reserve))
+                              COMM_RESERVE_BLOCKS if comm_reserve is None else int(comm_reserve),
+                              self.out == "u8" if rows is None else bool(rows) and self.out == "u8")
             return
         # zero-filled once: the padding beyond a short part's tile is sent but never read
         self.send = [torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]
@@ -127,7 +131,7 @@ class TileGather:
         self._recv_lists = [list(b.unbind(0)) for b in self.recv] if self.recv is not None else None
         self._views = [b[:self.n].view(self.shape) for b in self.send]
 
-    def _init_native(self, dtype, plen, slots, persistent_frames, loop, reserve) -> None:
+    def _init_native(self, dtype, plen, slots, persistent_frames, loop, reserve, rows) -> None:
         import ctypes
 
         from python_ray_tracer_amd.infrastructure.hip import _lib as L
@@ -139,8 +143,11 @@ class TileGather:
         root = self.rank == self.dst
         self.send = ([torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]
                      if not root or loop else [])
-        self.recv = ([torch.zeros((self.world, plen), dtype=dtype, device=self.device) for _ in range(slots)]
-                     if root and (self.world > 1 or loop) else None)
+        gathers = self.world > 1 or loop
+        self.rows = rows and gathers
+        # RTX_TILES_ROWS: the root keeps only its own tile (the peers' blocks land in the frame)
+        self.recv = ([torch.zeros((1 if self.rows else self.world, plen), dtype=dtype, device=self.device)
+                      for _ in range(slots)] if root and gathers else None)
         self.frame_shape = (self.H, self.W, 3) if self.out == "u8" else (3, self.H * self.W)
         self._dtype = dtype
         self.frames = ([torch.empty(self.frame_shape, dtype=dtype, device=self.device) for _ in range(slots)]
@@ -154,7 +161,8 @@ class TileGather:
         with torch.cuda.device(self.device):
             L.check(self._lib.rtx_tiles_create(comm, self.world, self.rank, self.dst, self.W, self.H, self.rb, kind,
                                                slots, send, recv, plen * torch.empty((), dtype=dtype).element_size(),
-                                               (L.TILES_LOOPBACK if loop else 0) | ((reserve & 0xFFF) << L.F_RESERVE_SHIFT),
+                                               (L.TILES_LOOPBACK if loop else 0) | (L.TILES_ROWS if self.rows else 0)
+                                               | ((reserve & 0xFFF) << L.F_RESERVE_SHIFT),
                                                ctypes.byref(plan)),
                     "rtx_tiles_create")
         self.plan = plan.value

@@ -97,6 +97,7 @@ EXPORTS = (
 
 TILES_MAX_SLOTS = 4
 TILES_LOOPBACK = 1  # rtx_tiles_create flags
+TILES_ROWS = 2
 UNIQUE_ID_BYTES = 128  # ncclUniqueId
 
 _c_void_p = ctypes.c_void_p

@@ -82,8 +82,9 @@ def test_nccl_two_slot_pipeline_equals_single_frames():
 
 def test_native_tiles_loopback_and_graph_replay():
     """The native row-tiled step (rtx_tiles_submit) on a one-rank RCCL group: (1) a loopback plan —
-    the tile sent to and received from the rank itself over RCCL, then assembled — gives the
-    single-GPU frames bit for bit through the two-slot pipeline; (2) a render_tile(into=) frame and
+    the tile sent to and received from the rank itself over RCCL, row block by row block straight
+    into the frame (RTX_TILES_ROWS) or whole and then assembled — gives the single-GPU frames bit
+    for bit through the two-slot pipeline; (2) a render_tile(into=) frame and
     a native tiles step captured into HIP graphs (include/rtx_hip.h: the entry points never
     allocate or synchronise) replay to the eager frames bit for bit."""
     if not torch.cuda.is_available():
@@ -102,18 +103,19 @@ def test_native_tiles_loopback_and_graph_replay():
         frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 9))) for k in range(5)]
         r = HipRenderer(max_bounces=4, color_dtype=torch.float32, device=dev)
         want = [r.render_tile(sc, out="u8").clone() for sc in frames]
-        tg = TileGather(r, 104, 57, row_block=8, out="u8", slots=2, loopback=True)
-        assert tg.plan is not None and tg.send and tg.recv is not None
-        got, open_slot = [], None
-        for k, sc in enumerate(frames):
-            tg.submit(sc, k % 2)
-            if open_slot is not None:
-                got.append(tg.finish(open_slot))
-            open_slot = k % 2
-        got.append(tg.finish(open_slot))
-        torch.cuda.synchronize()
-        for k in range(len(frames)):
-            assert torch.equal(got[k], want[k]), k
+        for rows in (True, False):  # row blocks straight into the frame (RTX_TILES_ROWS), or assembled
+            tg = TileGather(r, 104, 57, row_block=8, out="u8", slots=2, loopback=True, rows=rows)
+            assert tg.plan is not None and tg.send and tg.recv is not None and tg.rows == rows
+            got, open_slot = [], None
+            for k, sc in enumerate(frames):
+                tg.submit(sc, k % 2)
+                if open_slot is not None:
+                    got.append(tg.finish(open_slot))
+                open_slot = k % 2
+            got.append(tg.finish(open_slot))
+            torch.cuda.synchronize()
+            for k in range(len(frames)):
+                assert torch.equal(got[k], want[k]), (rows, k)
 
         sc = frames[3]
         buf = torch.empty_like(want[3])
