@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B session on the GPU box: GPU tests on the default build, then tools/ab.py over configs.
-# Usage: bash tools/ab_run.sh <tag> <configs (comma list)> <lib.so>...   (env: AB_ROUNDS, AB_ITERS, AB_BOUNCES)
+# Usage: bash tools/sessions/ab_run.sh <tag> <configs (comma list)> <lib.so>...   (env: AB_ROUNDS, AB_ITERS, AB_BOUNCES)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -2,4 +2,4 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-AB_TESTS=0 bash tools/ab_run.sh ${ABL_TAG:-abl} ${ABL_CFGS:-C2,C2main,C3} "$@" 2>&1 | grep -E "median|=="
+AB_TESTS=0 bash tools/sessions/ab_run.sh ${ABL_TAG:-abl} ${ABL_CFGS:-C2,C2main,C3} "$@" 2>&1 | grep -E "median|=="

@@ -13,4 +13,4 @@ run emul_plain 300 python bench.py --config C4 --emulate-parts 8 --steps 20 --no
 run emul_nooct 300 python bench.py --config C4 --emulate-parts 8 --steps 20 --no-octant-tree --json-out $O/emul_C4_nooct.json
 run bench_C4 300 python bench.py --config C4 --steps 30 --warmup 3 --cpu-seconds 0 --json-out $O/bench_C4.json
 run bench_C4_nooct 300 python bench.py --config C4 --steps 30 --warmup 3 --cpu-seconds 0 --no-secondary --no-octant-tree --json-out $O/bench_C4_nooct.json
-bash tools/gpu_trace_session.sh r4b_trace "C4,8,0 C4,1,0 C2,1,0"
+bash tools/sessions/gpu_trace_session.sh r4b_trace "C4,8,0 C4,1,0 C2,1,0"

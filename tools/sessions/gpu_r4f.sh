@@ -21,3 +21,11 @@ for v in c2_base c2_w1 c2_w2; do
   RTX_HIP_LIB=ab/$v.so run ${v}_plain 120 python bench.py $B --no-tile-order --json-out $O/${v}_plain.json
 done
 run bench_default 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 0 --json-out $O/bench_default.json
+# C3: 5 waves with spills (base) against 4 waves without (kLvWaves=4); C4: B=5 at 4 waves with two LDS
+# level slots (base, 47 spilled VGPRs) against 3 waves with three (no spills)
+for v in c3_base c3_lv4 c3_base; do
+  RTX_HIP_LIB=ab/$v.so run ${v}_C3 200 python bench.py --config C3 --steps 100 --warmup 10 --cpu-seconds 0 --no-secondary --json-out $O/${v}_C3.json
+done
+for v in c4_base c4_b5s3 c4_base; do
+  RTX_HIP_LIB=ab/$v.so run ${v}_C4 200 python bench.py --config C4 --steps 30 --warmup 3 --cpu-seconds 0 --no-secondary --json-out $O/${v}_C4.json
+done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Tile-trace session on the GPU box (tools/tile_trace.py over a library built with the tile_trace
 # instrument: python tools/ab_build.py ab/trace.so --patch tile_trace --only-b 3,4,5).
-# Usage: bash tools/gpu_trace_session.sh <tag> "<config parts part> ..."
+# Usage: bash tools/sessions/gpu_trace_session.sh <tag> "<config parts part> ..."
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Dynamic instruction counts of several library builds (one rocprofv3 --pmc run per build and
 # counter group). Usage on the GPU box:
-#   bash tools/pmc_ab.sh <tag> <config> <lib.so>...
+#   bash tools/sessions/pmc_ab.sh <tag> <config> <lib.so>...
 # Summaries: python tools/pmc_summary.py gpurun_out/<tag>/<lib-name>
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
