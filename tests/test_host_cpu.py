@@ -91,6 +91,40 @@ def test_workspace_bytes_and_error_paths():
     assert lib.rtx_sphere_intersect(None, None, 0, None, 5, None, None) == -1
 
 
+def test_sched_and_tiles_entry_points_validate_on_host():
+    """The dispatch-order and row-tiled-frame entry points (round 4): unit counts of a launch, and
+    the argument checks that run before any HIP or RCCL call (no GPU needed)."""
+    lib = L.load()
+    text = (REPO / "include" / "rtx_hip.h").read_text()
+    for name, val in (("RTX_TILES_LOOPBACK", L.TILES_LOOPBACK), ("RTX_TILES_ROWS", L.TILES_ROWS),
+                      ("RTX_F_RESERVE_SHIFT", L.F_RESERVE_SHIFT), ("RTX_TILES_MAX_SLOTS", L.TILES_MAX_SLOTS)):
+        assert int(re.search(rf"#define\s+{name}\s+(\d+)", text).group(1)) == val, name
+    n = ctypes.c_int64()
+    # a persistent launch (>= 32 spheres) hands out 8x8 wave tiles
+    assert lib.rtx_sched_tiles(7680, 4320, 65, ctypes.byref(n)) == 0 and n.value == 960 * 540
+    # below 8 spheres: block tiles of 2x2 waves of 16x4 pixels (32 x 8)
+    assert lib.rtx_sched_tiles(1920, 1080, 3, ctypes.byref(n)) == 0 and n.value == 60 * 135
+    # 8..31 spheres: block tiles of 4x1 waves of 8x8 pixels (32 x 8)
+    assert lib.rtx_sched_tiles(3840, 2160, 17, ctypes.byref(n)) == 0 and n.value == 120 * 270
+    assert lib.rtx_sched_tiles(1920, 0, 3, ctypes.byref(n)) == 0 and n.value == 0
+    # unknown flag bits are refused before anything is launched
+    rc = lib.rtx_render_camera_sched(None, 3, 16, 16, 1, 1, 0, 16, 3, None, 0, None, 0, None, None, 1 << 20, None,
+                                     None, None)
+    assert rc == -1 and b"flags" in lib.rtx_last_error()
+    plan = ctypes.c_void_p()
+    ptrs = (ctypes.c_void_p * 2)(1, 1)
+    # a gathering plan needs a communicator (RTX_E_COMM); RTX_TILES_ROWS needs uint8 frames
+    assert lib.rtx_tiles_create(None, 2, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, ptrs, ptrs, 4096, 0, ctypes.byref(plan)) == -4
+    assert lib.rtx_tiles_create(None, 2, 0, 0, 64, 64, 8, L.OUT_F32_SOA, 2, ptrs, ptrs, 8192, L.TILES_ROWS,
+                                ctypes.byref(plan)) == -1
+    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 9, None, None, 16, 0, ctypes.byref(plan)) == -1
+    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, None, None, 16, 1 << 20,
+                                ctypes.byref(plan)) == -1
+    assert plan.value is None
+    assert lib.rtx_tiles_submit(None, 0, None, 3, 3, None, 0, 0, None, None, None, None, None) == -1
+    assert lib.rtx_tiles_destroy(None) == 0
+
+
 def test_pack_matches_reference_expressions():
     spec = scenes.readme_spec(160, 90)
     sc = scenes.build_scene(spec)  # HipSphere & co. need no GPU to construct
