@@ -86,9 +86,9 @@ def parse():
     ap.add_argument("--comm-reserve", type=int, default=None,
                     help="tiles mode: block slots a gathering plan's persistent renders leave free for the RCCL "
                          "kernels of the previous frame (default distributed.COMM_RESERVE_BLOCKS)")
-    ap.add_argument("--assemble", action="store_true",
-                    help="tiles mode: gather whole tiles and assemble them on the root instead of moving each row "
-                         "block straight into the root's frame (RTX_TILES_ROWS, the uint8 default) (A/B)")
+    ap.add_argument("--rows", action="store_true",
+                    help="tiles mode: move each row block straight into the root's frame (RTX_TILES_ROWS) instead "
+                         "of gathering whole tiles and assembling them on the root (A/B)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -165,7 +165,7 @@ def main():
                                     device_id=dev)
         step, drain = tiles_stepper(r, scene, world, args.row_block, "u8" if args.out == "u8" else None,
                                     loopback=args.loopback, comm_reserve=args.comm_reserve,
-                                    rows=False if args.assemble else None)
+                                    rows=args.rows)
         px_per_step = W * H
 
     def barrier():  # every rank's queued GPU work done, then all ranks meet

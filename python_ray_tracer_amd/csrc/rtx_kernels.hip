@@ -53,7 +53,11 @@ constexpr int kWaveW = 8;       // pixels per wave row: a wave renders a kWaveW 
 // C2 -0.8%, C2main -1.1%, C1 -6%; the culled kernels keep 8 x 8: C5 +0.6%, C4 +3% at 16 x 4, the
 // wave frustum and beam bounds are tighter on square tiles)
 constexpr int kWaveWSmall = 16;
-constexpr int kFastWaves = 4;   // waves per k_render_fast block (1, 2 or 4)
+constexpr int kFastWaves = 4;   // waves per k_render_fast block (1, 2 or 4) of the culled kernels
+// ... and of the TREE = false kernels (scenes below kTreeMinSpheres): one wave per block, so the
+// hardware hands out single 16x4 wave tiles in the learnt longest-first order (rtx_render_camera_sched;
+// A/B r4f, C2: 52.8 against 54.5 us per frame with four-wave blocks, 54.7 / 55.7 without the order)
+constexpr int kFastWavesSmall = 1;
 // k_render_fast single-frame launches of scenes with at least this many spheres: persistent waves
 // fetching wave tiles (A/B: 65 spheres -14%, 17 spheres +-0, 3-16 spheres without the culling tree
 // +12%: their tiles are short, so the ramp-up of the fetch counters and the drain cost more than
@@ -90,16 +94,21 @@ constexpr int kShadeMath = 3;
 // ---- derived ----
 constexpr int kWaveH = 64 / kWaveW;
 static_assert(kFastWaves == 1 || kFastWaves == 2 || kFastWaves == 4, "kFastWaves");
+static_assert(kFastWavesSmall == 1 || kFastWavesSmall == 2 || kFastWavesSmall == 4, "kFastWavesSmall");
 static_assert((kMaxFetch & (kMaxFetch - 1)) == 0, "kMaxFetch must be a power of two");
 constexpr int kFastBlock = 64 * kFastWaves;
-constexpr int kWavesX = kFastWaves == 1 ? 1 : 2;  // block tile: kWavesX x kWavesY waves
+constexpr int kWavesX = kFastWavesSmall == 1 ? 1 : 2;  // block tile of the small kernels: kWavesX x kWavesY waves
 constexpr int kWavesXTree = kFastWaves;  // ... of the culled kernels: one row of waves (A/B r3o: C5 -3.0%, C3 +-0.3%; C1 +9% for the small ones)
 static_assert(kWaveWSmall > 0 && kWaveWSmall <= 64 && 64 % kWaveWSmall == 0, "kWaveWSmall");
 template <bool TREE>
 __host__ __device__ constexpr int wave_w() { return TREE ? kWaveW : kWaveWSmall; }
 template <bool TREE>
 __host__ __device__ constexpr int waves_x() { return TREE ? kWavesXTree : kWavesX; }
-static_assert(kFastWaves % kWavesX == 0 && kFastWaves % kWavesXTree == 0, "block wave layout");
+template <bool TREE>
+__host__ __device__ constexpr int fast_waves() { return TREE ? kFastWaves : kFastWavesSmall; }
+template <bool TREE>
+__host__ __device__ constexpr int fast_block() { return 64 * fast_waves<TREE>(); }
+static_assert(kFastWavesSmall % kWavesX == 0 && kFastWaves % kWavesXTree == 0, "block wave layout");
 constexpr int kFrameWords = 20;  // general-kernel stack frame (float64 words)
 constexpr int kFetchStride = 32;  // uint32 words between counters
 constexpr int kSphWords = RTX_GEOM_WORDS + RTX_MAT_WORDS;
@@ -114,8 +123,10 @@ template <bool DEEP = false>
 __host__ __device__ constexpr int level_lds_slots(int B) {
   return DEEP || B < kLevelsLdsSlots ? B : B >= 5 ? kB5Slots : kLevelsLdsSlots;
 }
-template <bool DEEP = false>
-__host__ __device__ constexpr size_t level_lds_bytes(int B) { return (size_t)level_lds_slots<DEEP>(B) * kFastBlock * (4 * 8 + 4); }
+template <bool DEEP = false, bool TREE = true>
+__host__ __device__ constexpr size_t level_lds_bytes(int B) {
+  return (size_t)level_lds_slots<DEEP>(B) * fast_block<TREE>() * (4 * 8 + 4);
+}
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
@@ -1559,6 +1570,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
+  constexpr int FB = fast_block<TREE>();  // threads per block of this instantiation
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
@@ -1573,17 +1585,17 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   if (p.mode == 0) {
     // WX x WY waves per block; wave w -> WW x WH sub-tile, lane -> (l % WW, l / WW)
     // (wave_tile: (bx, by) is this wave's own WW x WH tile; TREE only, so WW = kWaveW there)
-    constexpr int WW = wave_w<TREE>(), WH = 64 / WW, WX = waves_x<TREE>(), WY = kFastWaves / WX;
+    constexpr int WW = wave_w<TREE>(), WH = 64 / WW, WX = waves_x<TREE>(), WY = fast_waves<TREE>() / WX;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     col = wave_tile ? bx * WW + (lane % WW) : bx * (WX * WW) + (w % WX) * WW + (lane % WW);
     lr = wave_tile ? by * WH + (lane / WW) : by * (WY * WH) + (w / WX) * WH + (lane / WW);
     active = col < p.width && lr < p.n_rows;
     i = (int64_t)lr * p.width + col;
   } else if (!DEEP || p.mode == 1 || p.mode == 3) {
-    i = (int64_t)bx * kFastBlock + threadIdx.x;
+    i = (int64_t)bx * FB + threadIdx.x;
     active = i < p.n;
   } else {  // continuation: entry `item` of in_list
-    const int64_t item = (int64_t)bx * kFastBlock + threadIdx.x;
+    const int64_t item = (int64_t)bx * FB + threadIdx.x;
     active = item < (int64_t)*p.in_count;
     if (active) {
       const uint64_t e = p.in_list[item];
@@ -1674,8 +1686,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   constexpr int NR = LV ? (B > NL ? B - NL : 1) : NS;
   double sDli[NR], sDi[NR], sSpec[NR], sVa[NR];
   int sKey[NR];  // hit sphere | checker bit << 16
-  double* const lvd = LV ? const_cast<double*>(lds_tab) + nsph * kSphWords : nullptr;  // [NL][4][kFastBlock]
-  int* const lvk = LV ? (int*)(lvd + NL * 4 * kFastBlock) : nullptr;                  // [NL][kFastBlock]
+  double* const lvd = LV ? const_cast<double*>(lds_tab) + nsph * kSphWords : nullptr;  // [NL][4][FB]
+  int* const lvk = LV ? (int*)(lvd + NL * 4 * FB) : nullptr;                          // [NL][FB]
   const int lt = threadIdx.x;
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
@@ -1731,10 +1743,10 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         if constexpr (LV) {  // LDS slot d = level kb + d (a DEEP kernel keeps all B levels there)
           static_assert(!LV || !DEEP || NL == B, "DEEP level slots");
           for (int d = 0; d < NL; ++d) {
-            const double* const l = lvd + (d * 4) * kFastBlock + lt;
+            const double* const l = lvd + (d * 4) * FB + lt;
             double* lj = rec + 6 + kRecLevelWords * (kb + d);
-            lj[0] = l[0]; lj[1] = l[kFastBlock]; lj[2] = l[2 * kFastBlock]; lj[3] = l[3 * kFastBlock];
-            lj[4] = (double)lvk[d * kFastBlock + lt];
+            lj[0] = l[0]; lj[1] = l[FB]; lj[2] = l[2 * FB]; lj[3] = l[3 * FB];
+            lj[4] = (double)lvk[d * FB + lt];
           }
         } else if constexpr (B > 0) {
 #pragma unroll
@@ -1756,9 +1768,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     // push this level's colour inputs; the reflected ray becomes the next level
     if constexpr (LV) {
       if (NL == B || k < NL) {  // k: wave-uniform, == depth of every active lane
-        double* const l = lvd + (depth * 4) * kFastBlock + lt;
-        l[0] = s.dli; l[kFastBlock] = s.di; l[2 * kFastBlock] = s.spec; l[3 * kFastBlock] = s.va;
-        lvk[depth * kFastBlock + lt] = level_key(hit, s.tk);
+        double* const l = lvd + (depth * 4) * FB + lt;
+        l[0] = s.dli; l[FB] = s.di; l[2 * FB] = s.spec; l[3 * FB] = s.va;
+        lvk[depth * FB + lt] = level_key(hit, s.tk);
       } else {  // levels beyond the LDS slots: a register shift (slot 0 = the most recent)
 #pragma unroll
         for (int j = NR - 1; j > 0; --j) {
@@ -1847,10 +1859,10 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       }
     }
     for (int d = (depth < NL ? depth : NL) - 1; d >= 0; --d) {
-      const double* const l = lvd + (d * 4) * kFastBlock + lt;
-      const int key = lvk[d * kFastBlock + lt];
-      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, l[0], l[kFastBlock], key_tex(key), true, true,
-                l[2 * kFastBlock], l[3 * kFastBlock], cr, cg, cb, cr, cg, cb);
+      const double* const l = lvd + (d * 4) * FB + lt;
+      const int key = lvk[d * FB + lt];
+      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, l[0], l[FB], key_tex(key), true, true,
+                l[2 * FB], l[3 * FB], cr, cg, cb, cr, cg, cb);
     }
   } else {
     for (int d = 0; d < depth; ++d) {
@@ -1878,8 +1890,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 // TP: 0 = no culling tree and no persistent launch (scenes below kTreeMinSpheres), 1 = culling tree,
 // one tile per block (the launch is not persistent), 2 = both (persistent launches)
 template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2>
-__global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
-                                                                   : kFastWavesPerSimd)) void k_render_fast(Params p0) {
+__global__ __launch_bounds__(fast_block<(TP >= 1)>(),
+                             (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
+                                                      : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   constexpr bool TREE = TP >= 1;
   // reflected-ray beams (wave_beam): scenes of kPersistMinSpheres and more, capped renders (A/B: C4
   // -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%)
@@ -1900,12 +1913,12 @@ __global__ __launch_bounds__(kFastBlock, (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
                         // in fast_tile, after the first tile's level-0 nearest-hit test)
     const double* src = p.scene + RTX_HDR_WORDS;
-    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += kFastBlock) lds_tab[k] = src[k];
+    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += fast_block<TREE>()) lds_tab[k] = src[k];
   }
   if constexpr (DEEP) {
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
-      for (int64_t t = blockIdx.x; t * kFastBlock < count; t += gridDim.x) {
+      for (int64_t t = blockIdx.x; t * fast_block<TREE>() < count; t += gridDim.x) {
         fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
@@ -2417,7 +2430,7 @@ void block_grid(int nsph, int width, int n_rows, int64_t& gx, int64_t& gy) {
   const bool small = nsph < kTreeMinSpheres;
   const int wx = small ? waves_x<false>() : waves_x<true>();
   const int tw = wx * (small ? wave_w<false>() : wave_w<true>());
-  const int th = (kFastWaves / wx) * (64 / (small ? wave_w<false>() : wave_w<true>()));
+  const int th = ((small ? fast_waves<false>() : fast_waves<true>()) / wx) * (64 / (small ? wave_w<false>() : wave_w<true>()));
   gx = (width + tw - 1) / tw;
   gy = (n_rows + th - 1) / th;
 }
@@ -2451,7 +2464,9 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
 // without the tree walks either (TP 0) (A/B in DESIGN.md §4).
 template <int B, bool DEEP, bool LVL, bool STATS>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
-  const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) + (LVL ? level_lds_bytes<DEEP>(B) : 0);
+  const bool small = p.nsph < kTreeMinSpheres;  // the TREE = false kernels: fast_block<false>() threads
+  const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
+                     (LVL ? (small ? level_lds_bytes<DEEP, false>(B) : level_lds_bytes<DEEP>(B)) : 0);
   if (p.n_fetch == 0) {  // one tile per block: the instantiations without the persistent loop
     if (p.nsph < kTreeMinSpheres) {  // TP 0: the rtx_small.hip unit
       const hipError_t e = rtx_launch_small(B, DEEP, LVL, STATS, &p, grid, (uint32_t)lds, s, prof_event(0), prof_event(1));
@@ -2557,7 +2572,8 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
     dim3 grid;
-    int64_t tx = (p.n + kFastBlock - 1) / kFastBlock, ty = 1;
+    const int64_t fb = p.nsph < kTreeMinSpheres ? fast_block<false>() : fast_block<true>();
+    int64_t tx = (p.n + fb - 1) / fb, ty = 1;
     if (p.mode == 0) block_grid(p.nsph, p.width, p.n_rows, tx, ty);
     p.n_fetch = 0;
     if (p.nsph >= kPersistMinSpheres && p.mode == 0 && p.n_frames == 1) {
@@ -2608,7 +2624,8 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
       q.drec_level = levels[pass];
       q.rec_cap = caps[pass];
       q.in_rec_cap = p.in_rec_cap;
-      const int64_t tiles = (n_all + kFastBlock - 1) / kFastBlock;
+      const int64_t fb = p.nsph < kTreeMinSpheres ? fast_block<false>() : fast_block<true>();
+      const int64_t tiles = (n_all + fb - 1) / fb;
       const int64_t cap = 4 * (int64_t)device_cus();
       launch_fast_deep(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
       if (int e = check_launch("k_render_fast (continuation)")) return e;

@@ -11,7 +11,8 @@ namespace {
 template <int B, bool DEEP, bool LVL, bool STATS>
 hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const Params& p = *static_cast<const Params*>(params);
-  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0>), grid, dim3(kFastBlock), lds, s, e0, e1, 0u, p);
+  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0>), grid, dim3(fast_block<false>()), lds, s, e0, e1,
+                        0u, p);
   return hipSuccess;  // launch errors reach the caller's check_launch through hipGetLastError
 }
 

@@ -93,8 +93,10 @@ class TileGather:
         (sent to and received from the rank itself), the gather path on one GPU (tests).
         ``comm_reserve``: block slots every persistent render of a gathering plan leaves free for the
         previous frame's RCCL kernels (RTX_F_RESERVE; default COMM_RESERVE_BLOCKS). ``rows`` (native,
-        uint8 frames; the default there): every row block travels on its own straight into the
-        root's frame (RTX_TILES_ROWS), with no assembly pass on the root."""
+        uint8 frames): every row block travels on its own straight into the root's frame
+        (RTX_TILES_ROWS), with no assembly pass on the root. Off by default: RCCL charges ~2.7 us per
+        operation (one GPU, C4 loopback: 5,480 us per step with row blocks of 8 rows, 2,837 with 32,
+        against 2,190 gathered whole and assembled)."""
         import torch.distributed as dist
 
         self._dist = dist
@@ -120,7 +122,7 @@ class TileGather:
         if native:
             self._init_native(dtype, plen, slots, persistent_frames, loopback and self.world == 1,
                               COMM_RESERVE_BLOCKS if comm_reserve is None else int(comm_reserve),
-                              self.out == "u8" if rows is None else bool(rows) and self.out == "u8")
+                              bool(rows) and self.out == "u8")
             return
         # zero-filled once: the padding beyond a short part's tile is sent but never read
         self.send = [torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]

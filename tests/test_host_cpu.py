@@ -102,8 +102,8 @@ def test_sched_and_tiles_entry_points_validate_on_host():
     n = ctypes.c_int64()
     # a persistent launch (>= 32 spheres) hands out 8x8 wave tiles
     assert lib.rtx_sched_tiles(7680, 4320, 65, ctypes.byref(n)) == 0 and n.value == 960 * 540
-    # below 8 spheres: block tiles of 2x2 waves of 16x4 pixels (32 x 8)
-    assert lib.rtx_sched_tiles(1920, 1080, 3, ctypes.byref(n)) == 0 and n.value == 60 * 135
+    # below 8 spheres: one-wave blocks of 16x4 pixels
+    assert lib.rtx_sched_tiles(1920, 1080, 3, ctypes.byref(n)) == 0 and n.value == 120 * 270
     # 8..31 spheres: block tiles of 4x1 waves of 8x8 pixels (32 x 8)
     assert lib.rtx_sched_tiles(3840, 2160, 17, ctypes.byref(n)) == 0 and n.value == 120 * 270
     assert lib.rtx_sched_tiles(1920, 0, 3, ctypes.byref(n)) == 0 and n.value == 0
