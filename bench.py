@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--rows", action="store_true",
                     help="tiles mode: move each row block straight into the root's frame (RTX_TILES_ROWS) instead "
                          "of gathering whole tiles and assembling them on the root (A/B)")
+    ap.add_argument("--shares", default=None, metavar="ROOT_RUN,RUN",
+                    help="--emulate-parts: the root renders ROOT_RUN parts and every other rank RUN parts of the "
+                         "interleave (default distributed.ROOT_SHARES by N)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU); gloo is a test mode for ranks sharing a GPU")
     return ap.parse_args()
@@ -501,8 +504,10 @@ def emulate_parts(args, r, scene, spec, B, part_counts):
     part_len] uint8 gather buffer, as rank p would, and timed — the fast kernel by the library's HIP
     events, the whole launch (fast + general kernel, host call) by wall clock over K synchronised
     launches — then rtx_assemble_rows of the N parts (the root's un-permute), whose frame must equal
-    the single-GPU render. The gather itself is not emulated: DESIGN.md §6 prices it from the part
-    bytes reported here."""
+    the single-GPU render. Each rank's share follows the plan's (--shares, else
+    distributed.ROOT_SHARES): the root renders root_run parts, every other rank run parts of the
+    root_run + (N-1)*run interleave. The gather itself is not emulated: DESIGN.md §6 prices it from
+    the part bytes reported here."""
     import numpy as np
     import torch
 
@@ -535,26 +540,32 @@ def emulate_parts(args, r, scene, spec, B, part_counts):
         return (time.perf_counter() - t0) / k * 1e6
 
     whole = r.render_tile(scene, out="u8")
+    from python_ray_tracer_amd.distributed import ROOT_SHARES
+
     res = {}
     for N in sorted({1, *part_counts}):
-        plen = tiling.part_len(H, W, rb, N, 1, "u8")
+        root_run, run = ((int(v) for v in args.shares.split(",")) if args.shares and N > 1
+                         else ROOT_SHARES.get(N, (1, 1)))
+        n_parts, shares = tiling.runs(N, root_run, run)
+        plen = tiling.part_len(H, W, rb, N, 1, "u8", root_run, run)
         tiles = torch.zeros((N, plen), dtype=torch.uint8, device=dev)
         parts = []
-        for p in range(N):
-            shp = tiling.tile_shape(H, W, rb, N, p, "u8")
+        for p, (first, k_run) in enumerate(shares):
+            shp = tiling.tile_shape(H, W, rb, n_parts, first, "u8", k_run)
             view = tiles[p, :int(np.prod(shp))].view(shp)
 
-            def fn(p=p, view=view):
-                return r.render_tile(scene, rb, N, p, out="u8", into=view)
-            parts.append({"part": p, "rows": shp[0], "kernel_us": round(kernel_us(fn), 3),
+            def fn(first=first, k_run=k_run, view=view):
+                return r.render_tile(scene, rb, n_parts, first, out="u8", into=view, part_run=k_run)
+            parts.append({"rank": p, "parts": [first, k_run], "rows": shp[0], "kernel_us": round(kernel_us(fn), 3),
                           "launch_us": round(wall_us(fn), 3)})
-        frame = r.assemble_rows(tiles, W, H, rb, "u8")
+        frame = r.assemble_rows(tiles, W, H, rb, "u8", root_run, run)
         if not torch.equal(frame, whole):
-            raise AssertionError(f"assembled {N}-part frame differs from the whole-frame render")
-        asm_us = wall_us(lambda: r.assemble_rows(tiles, W, H, rb, "u8"))
+            raise AssertionError(f"assembled {N}-rank frame differs from the whole-frame render")
+        asm_us = wall_us(lambda: r.assemble_rows(tiles, W, H, rb, "u8", root_run, run))
         kus = [q["kernel_us"] for q in parts]
         lus = [q["launch_us"] for q in parts]
-        res[str(N)] = {"kernel_us_max": max(kus), "kernel_us_mean": round(sum(kus) / N, 3),
+        res[str(N)] = {"shares": [root_run, run], "kernel_us_max": max(kus), "kernel_us_mean": round(sum(kus) / N, 3),
+                       "root_kernel_us": kus[0], "peer_kernel_us_max": max(kus[1:]) if N > 1 else None,
                        "imbalance": round(max(kus) / (sum(kus) / N), 4), "launch_us_max": max(lus),
                        "assemble_us": round(asm_us, 3), "part_bytes": plen, "root_receives_bytes": (N - 1) * plen,
                        "frame_equals_single_gpu": True, "parts": parts}

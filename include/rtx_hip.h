@@ -263,7 +263,12 @@ int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int heig
                          void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream,
                          unsigned flags, uint32_t* deferred_out);
 
-/* rtx_render_camera_ex with a dispatch order. A camera launch of one frame (or row tile) is
+/* rtx_render_camera_ex with a run of parts and a dispatch order.
+ * part_run >= 1: the local rows of parts part .. part + part_run - 1 of the n_parts interleave as one
+ * tile (part_run * row_block rows of every cycle of n_parts * row_block rows; local row lr is global
+ * row (lr / (part_run row_block)) n_parts row_block + part row_block + lr % (part_run row_block)),
+ * so a rank can take a larger or smaller share of the frame than 1 / n_parts.
+ * A camera launch of one frame (or row tile) is
  * dispatched in units: scenes of >= 32 spheres run persistent waves fetching kWaveW x kWaveH (8 x 8)
  * wave tiles from counters; smaller scenes one block tile (4 waves) per block, blocks dispatched in
  * grid order. rtx_sched_tiles gives the number of units; unit t is column t % units_x, row
@@ -277,7 +282,7 @@ int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int heig
  *    of the next identical launch. */
 int rtx_sched_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles);
 int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int height,
-                            int row_block, int n_parts, int part, int n_local_rows,
+                            int row_block, int n_parts, int part, int part_run, int n_local_rows,
                             int max_bounces, void* out, int out_kind,
                             void* workspace, size_t workspace_bytes, uint64_t* stats, void* stream,
                             unsigned flags, uint32_t* deferred_out, const uint32_t* tile_order,
@@ -335,6 +340,12 @@ int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, 
  * (the largest). */
 int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts, int width, int height,
                       int row_block, int kind, void* out, void* stream);
+/* rtx_assemble_rows for ranks that render runs of parts (rtx_render_camera_sched part_run): rank 0
+ * renders parts [0, root_run), rank i >= 1 parts [root_run + (i - 1) run, root_run + i run) of the
+ * root_run + (n_ranks - 1) run interleave; rank i's tile at tiles + i * part_stride_bytes (which
+ * must hold the longest run's tile). root_run == run == 1 is rtx_assemble_rows. */
+int rtx_assemble_runs(const void* tiles, int64_t part_stride_bytes, int n_ranks, int root_run, int run, int width,
+                      int height, int row_block, int kind, void* out, void* stream);
 
 /* ---- the row-tiled multi-GPU frame, one call per frame and rank (csrc/rtx_tiles.hip) ----
  * The north star's "framebuffer row-tiles across the GPUs of one node with an RCCL gather over
@@ -366,16 +377,21 @@ int rtx_comm_destroy(void* comm);
  * copy), so the root never runs the assembly pass (a read and a write of the whole frame in HBM,
  * beside its next render). recv[s] then holds the root's own tile only (part_bytes). */
 #define RTX_TILES_ROWS 2u
-/* A plan for frames of width x height in row blocks of row_block, out_kind RTX_OUT_*, `slots`
+/* Shares: rank 0 renders the run of parts [0, root_run) and rank i >= 1 the run [root_run + (i - 1)
+ * run, root_run + i run) of the root_run + (world - 1) run interleave (rtx_render_camera_sched
+ * part_run). root_run = run = 1 is the even split; a root_run below run leaves the root, which also
+ * receives and assembles every frame, a smaller share (then the root must be rank 0). part_bytes must
+ * hold the longest run's tile.
+ * A plan for frames of width x height in row blocks of row_block, out_kind RTX_OUT_*, `slots`
  * frames in flight (<= RTX_TILES_MAX_SLOTS). Per slot s, caller-owned device buffers kept for the
  * plan's life: a peer's send[s] (part_bytes) and the root's recv[s] (world * part_bytes: part p at
- * p * part_bytes). part_bytes holds part 0's tile (the largest), a multiple of 16. world == 1 needs
+ * p * part_bytes). part_bytes holds the longest run's tile, a multiple of 16. world == 1 needs
  * neither buffers nor a communicator (comm NULL): the single part is the frame (unless
  * RTX_TILES_LOOPBACK: then send and recv as a root and peer would). Creates the plan's own
  * collective stream on the current device. */
 int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int height, int row_block, int out_kind,
-                     int slots, void* const* send, void* const* recv, int64_t part_bytes, unsigned flags,
-                     void** plan_out);
+                     int slots, void* const* send, void* const* recv, int64_t part_bytes, int root_run, int run,
+                     unsigned flags, void** plan_out);
 /* Frame of slot `slot`: on `stream`, wait until the slot's previous frame has left its buffers, then
  * render this rank's tile (scene, n_spheres, max_bounces, workspace, flags, deferred_out, tile_order,
  * tile_cost as rtx_render_camera_sched); then, on the plan's stream after the render, the RCCL gather to the root

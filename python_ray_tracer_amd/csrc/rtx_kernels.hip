@@ -144,8 +144,9 @@ struct Params {
   int nsph;
   int mode;  // 0: camera rays, 1: explicit rays, 2: continuation of deferred chains (in_list),
              // 3: explicit rays whose level-0 hit is given (hit_shape at hit_t: Shader.create)
-  // camera mode
+  // camera mode: local rows of parts part .. part + part_run - 1 of the n_parts-way row interleave
   int width, height, row_block, n_parts, part, n_rows;
+  int part_run;
   // explicit-ray mode
   const double* org;
   int64_t org_stride;
@@ -1244,7 +1245,10 @@ __device__ __forceinline__ void reflect_dir(double& dx, double& dy, double& dz, 
 
 __device__ __forceinline__ int global_row(const Params& p, int lr) {
   if (p.n_parts == 1) return lr;  // a whole frame (uniform branch: no integer divisions)
-  return ((lr / p.row_block) * p.n_parts + p.part) * p.row_block + (lr % p.row_block);
+  // a run of part_run consecutive parts owns part_run * row_block consecutive rows of every cycle of
+  // n_parts * row_block rows, from row part * row_block of the cycle (part_run == 1: one row block)
+  const int own = p.row_block * p.part_run;
+  return (lr / own) * (p.n_parts * p.row_block) + p.part * p.row_block + (lr % own);
 }
 
 // get_ray_directions (base.py:123-141) for pixel (col, global row r).
@@ -2249,27 +2253,41 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const T* __restrict__ c, in
   out[3 * i + 2] = quant_u8((double)c[2 * n + i]);
 }
 
-// Rows of part p of the interleaved row tiling (python_ray_tracer_amd/tiling.py n_local_rows).
-__host__ __device__ __forceinline__ int tile_local_rows(int height, int row_block, int n_parts, int p) {
-  const int cycle = row_block * n_parts;
+// Rows of the run of `run` parts from part p of the interleaved row tiling (python_ray_tracer_amd/
+// tiling.py n_local_rows): run * row_block rows of every cycle, the last cycle's prefix.
+__host__ __device__ __forceinline__ int tile_local_rows(int height, int row_block, int n_parts, int p, int run = 1) {
+  const int cycle = row_block * n_parts, own = row_block * run;
   const int q = height / cycle, rem = height % cycle - p * row_block;
-  return q * row_block + (rem < 0 ? 0 : rem > row_block ? row_block : rem);
+  return q * own + (rem < 0 ? 0 : rem > own ? own : rem);
+}
+// The rank that owns block-in-cycle b when rank 0 runs parts [0, root_run) and rank i >= 1 parts
+// [root_run + (i - 1) run, root_run + i run): its index, first part and run length.
+__host__ __device__ __forceinline__ void run_owner(int b, int root_run, int run, int& rank, int& first, int& len) {
+  if (b < root_run) {
+    rank = 0, first = 0, len = root_run;
+  } else {
+    rank = 1 + (b - root_run) / run, first = root_run + (rank - 1) * run, len = run;
+  }
 }
 
 // Un-permute of gathered row tiles (the multi-GPU frame, application.render_frame_distributed):
-// part p's buffer (at tiles + p * part_stride) holds its rows in local order, as rtx_render_camera
-// wrote them, [planes][rows_p][row_bytes]; the frame is [planes][height][row_bytes]. One block per
-// (frame row, plane): a contiguous row copy, 16 B per lane when the row and buffers allow it.
+// rank r's buffer (at tiles + r * part_stride) holds the rows of its run of parts in local order, as
+// rtx_render_camera_sched wrote them, [planes][rows_r][row_bytes]; the frame is
+// [planes][height][row_bytes]. One block per (frame row, plane): a contiguous row copy, 16 B per
+// lane when the row and buffers allow it.
 __global__ __launch_bounds__(kBlock) void k_assemble_rows(const uint8_t* __restrict__ tiles, int64_t part_stride,
-                                                          int n_parts, int height, int row_block, int64_t row_bytes,
-                                                          bool vec16, uint8_t* __restrict__ out) {
+                                                          int n_parts, int root_run, int run, int height,
+                                                          int row_block, int64_t row_bytes, bool vec16,
+                                                          uint8_t* __restrict__ out) {
   const int g = blockIdx.x;  // frame row
   const int c = blockIdx.y;  // plane
-  const int b = g / row_block;
-  const int p = b % n_parts;
-  const int lr = (b / n_parts) * row_block + g % row_block;
-  const int rows_p = tile_local_rows(height, row_block, n_parts, p);
-  const uint8_t* src = tiles + p * part_stride + ((int64_t)c * rows_p + lr) * row_bytes;
+  const int cyc = n_parts * row_block;
+  const int pos = g % cyc;
+  int r, first, len;
+  run_owner(pos / row_block, root_run, run, r, first, len);
+  const int lr = (g / cyc) * len * row_block + pos - first * row_block;
+  const int rows_r = tile_local_rows(height, row_block, n_parts, first, len);
+  const uint8_t* src = tiles + r * part_stride + ((int64_t)c * rows_r + lr) * row_bytes;
   uint8_t* dst = out + ((int64_t)c * height + g) * row_bytes;
   if (vec16) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -2719,13 +2737,14 @@ int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int heig
                          int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
                          size_t workspace_bytes, uint64_t* stats, void* stream, unsigned flags,
                          uint32_t* deferred_out) {
-  return rtx_render_camera_sched(scene, n_spheres, width, height, row_block, n_parts, part, n_local_rows,
+  return rtx_render_camera_sched(scene, n_spheres, width, height, row_block, n_parts, part, 1, n_local_rows,
                                  max_bounces, out, out_kind, workspace, workspace_bytes, stats, stream, flags,
                                  deferred_out, nullptr, nullptr);
 }
 
 int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,
-                            int part, int n_local_rows, int max_bounces, void* out, int out_kind, void* workspace,
+                            int part, int part_run, int n_local_rows, int max_bounces, void* out, int out_kind,
+                            void* workspace,
                             size_t workspace_bytes, uint64_t* stats, void* stream, unsigned flags,
                             uint32_t* deferred_out, const uint32_t* tile_order, uint32_t* tile_cost) {
   if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
@@ -2887,8 +2906,15 @@ int rtx_quantize_u8(const void* color, int color_kind, int64_t n, uint8_t* out, 
 
 int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts, int width, int height,
                       int row_block, int kind, void* out, void* stream) {
+  return rtx_assemble_runs(tiles, part_stride_bytes, n_parts, 1, 1, width, height, row_block, kind, out, stream);
+}
+
+int rtx_assemble_runs(const void* tiles, int64_t part_stride_bytes, int n_ranks, int root_run, int run, int width,
+                      int height, int row_block, int kind, void* out, void* stream) {
   if (!tiles || !out) return fail(RTX_E_ARG, "null pointer argument%s", "");
-  if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0) return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  if (width <= 0 || height <= 0 || row_block <= 0 || n_ranks <= 0 || root_run <= 0 || run <= 0)
+    return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
+  const int n_parts = root_run + (n_ranks - 1) * run;
   int planes = 3;
   int64_t row_bytes;
   if (kind == RTX_OUT_F32_SOA) {
@@ -2901,14 +2927,19 @@ int rtx_assemble_rows(const void* tiles, int64_t part_stride_bytes, int n_parts,
   } else {
     return fail(RTX_E_ARG, "bad kind%s %lld", "", kind);
   }
-  const int rmax = tile_local_rows(height, row_block, n_parts, 0);  // part 0 has the most rows
+  int rmax = 0;  // the longest run's rows
+  for (int r = 0; r < n_ranks; ++r) {
+    const int len = r == 0 ? root_run : run, first = r == 0 ? 0 : root_run + (r - 1) * run;
+    const int rows = tile_local_rows(height, row_block, n_parts, first, len);
+    rmax = rows > rmax ? rows : rmax;
+  }
   if (part_stride_bytes < planes * rmax * row_bytes)
     return fail(RTX_E_ARG, "part_stride too small%s (need %lld bytes)", "", (long long)(planes * rmax * row_bytes));
   const bool vec16 = row_bytes % 16 == 0 && part_stride_bytes % 16 == 0 && (uintptr_t)tiles % 16 == 0 &&
                      (uintptr_t)out % 16 == 0;
   hipLaunchKernelGGL(k_assemble_rows, dim3((unsigned)height, (unsigned)planes), dim3(kBlock), 0, (hipStream_t)stream,
-                     (const uint8_t*)tiles, part_stride_bytes, n_parts, height, row_block, row_bytes, vec16,
-                     (uint8_t*)out);
+                     (const uint8_t*)tiles, part_stride_bytes, n_parts, root_run, run, height, row_block, row_bytes,
+                     vec16, (uint8_t*)out);
   return check_launch("k_assemble_rows");
 }
 

@@ -72,6 +72,8 @@ struct Tiles {
   ncclComm_t comm;
   int world, rank, root;
   int width, height, row_block, out_kind;
+  int root_run, run;  // rank 0 renders parts [0, root_run), rank i parts [root_run + (i-1) run, + run)
+  int n_parts, first, my_run;  // the interleave (root_run + (world - 1) run parts) and this rank's run
   int slots;
   int64_t part_bytes;
   int local_rows;
@@ -87,10 +89,10 @@ struct Tiles {
   bool used[RTX_TILES_MAX_SLOTS];
 };
 
-int local_rows(int height, int row_block, int n_parts, int p) {  // tiling.n_local_rows
-  const int cycle = row_block * n_parts;
+int local_rows(int height, int row_block, int n_parts, int p, int run = 1) {  // tiling.n_local_rows
+  const int cycle = row_block * n_parts, own = row_block * run;
   const int q = height / cycle, rem = height % cycle - p * row_block;
-  return q * row_block + (rem < 0 ? 0 : rem > row_block ? row_block : rem);
+  return q * own + (rem < 0 ? 0 : rem > own ? own : rem);
 }
 
 int64_t bytes_per_pixel(int kind) { return kind == RTX_OUT_F32_SOA ? 12 : kind == RTX_OUT_F64_SOA ? 24 : 3; }
@@ -211,8 +213,8 @@ int rtx_comm_destroy(void* comm) {
 }
 
 int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int height, int row_block, int out_kind,
-                     int slots, void* const* send, void* const* recv, int64_t part_bytes, unsigned flags,
-                     void** plan_out) {
+                     int slots, void* const* send, void* const* recv, int64_t part_bytes, int root_run, int run,
+                     unsigned flags, void** plan_out) {
   if (!plan_out) return err(RTX_E_ARG, "null plan pointer%s", "");
   *plan_out = nullptr;
   if (world < 1 || rank < 0 || rank >= world || root < 0 || root >= world)
@@ -228,8 +230,17 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
     return err(RTX_E_ARG, "RTX_TILES_ROWS needs uint8 frames (a row block is contiguous there)%s", "");
   if ((world > 1 || loop) && (!comm || !rccl_ready()))
     return err(RTX_E_COMM, "world > 1 (or a loopback plan) needs an RCCL communicator%s", "");
-  const int rows0 = local_rows(height, row_block, world, 0);  // part 0 has the most rows
-  if (part_bytes < rows0 * (int64_t)width * bytes_per_pixel(out_kind) || part_bytes % 16 != 0)
+  if (root_run < 1 || run < 1 || (world == 1 && (root_run != 1 || run != 1)) || (root != 0 && root_run != run))
+    return err(RTX_E_ARG, "bad runs%s (root_run %lld)", "", root_run);
+  if (rows && (root_run != 1 || run != 1)) return err(RTX_E_ARG, "RTX_TILES_ROWS needs runs of one part%s", "");
+  const int np = root_run + (world - 1) * run;
+  int rows_max = 0;  // the longest run's tile
+  for (int r = 0; r < world; ++r) {
+    const int n = r == 0 ? local_rows(height, row_block, np, 0, root_run)
+                         : local_rows(height, row_block, np, root_run + (r - 1) * run, run);
+    rows_max = n > rows_max ? n : rows_max;
+  }
+  if (part_bytes < rows_max * (int64_t)width * bytes_per_pixel(out_kind) || part_bytes % 16 != 0)
     return err(RTX_E_ARG, "part_bytes must hold part 0's tile and be a multiple of 16%s (%lld)", "", part_bytes);
   for (int s = 0; s < slots; ++s) {
     if (rank == root && (world > 1 || loop) && (!recv || !recv[s]))
@@ -248,7 +259,13 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   t->out_kind = out_kind;
   t->slots = slots;
   t->part_bytes = part_bytes;
-  t->local_rows = local_rows(height, row_block, world, rank);
+  t->root_run = root_run;
+  t->run = run;
+  t->n_parts = np;
+  // uniform runs (root_run == run) keep rank order whatever the root; otherwise the root is rank 0
+  t->first = rank == 0 ? 0 : root_run + (rank - 1) * run;
+  t->my_run = rank == 0 ? root_run : run;
+  t->local_rows = local_rows(height, row_block, np, t->first, t->my_run);
   t->loop = loop;
   t->rows = rows;
   t->reserve = (world > 1 || loop) ? (flags & RTX_F_RESERVE(0xFFF)) : 0u;
@@ -291,8 +308,8 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
               : t->world == 1 ? frame
               : root          ? (uint8_t*)t->recv[slot] + (t->rows ? 0 : (int64_t)t->root * t->part_bytes)
                               : t->send[slot];
-  if (int rc = rtx_render_camera_sched(scene, n_spheres, t->width, t->height, t->row_block, t->world, t->rank,
-                                       t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes,
+  if (int rc = rtx_render_camera_sched(scene, n_spheres, t->width, t->height, t->row_block, t->n_parts, t->first,
+                                       t->my_run, t->local_rows, max_bounces, dst, t->out_kind, workspace, workspace_bytes,
                                        nullptr, stream, flags | t->reserve, deferred_out, tile_order, tile_cost))
     return rc;
   if (single) return RTX_OK;
@@ -318,8 +335,8 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
   if (r != ncclSuccess) return nccl_err(root ? "ncclRecv" : "ncclSend", r);
   if (r2 != ncclSuccess) return nccl_err("ncclGroupEnd", r2);
   if (root) {
-    if (int rc = rtx_assemble_rows(t->recv[slot], t->part_bytes, t->world, t->width, t->height, t->row_block,
-                                   t->out_kind, frame, t->cs))
+    if (int rc = rtx_assemble_runs(t->recv[slot], t->part_bytes, t->world, t->root_run, t->run, t->width, t->height,
+                                   t->row_block, t->out_kind, frame, t->cs))
       return rc;
   }
   if ((e = hipEventRecord(t->done[slot], t->cs))) return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));

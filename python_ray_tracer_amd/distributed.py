@@ -40,6 +40,13 @@ from python_ray_tracer_amd import tiling
 COMM_RESERVE_BLOCKS = 64
 
 
+# Shares (root_run, run) of the row-tiled frame by world size: the root also receives every part and
+# assembles the frame beside its next render, so from 4 ranks on it renders one part where every
+# other rank renders two (the root's share that balances its render plus that traffic
+# against a peer's render is ~6-8% of the frame at 8 ranks, 1/15 here).
+ROOT_SHARES = {4: (1, 2), 5: (1, 2), 6: (1, 2), 7: (1, 2), 8: (1, 2)}
+
+
 # RCCL communicators of the native path, one per (process group, rank, device): creating one costs
 # a rendezvous, so TileGathers of the same group share it for the life of the process
 _COMMS: dict = {}
@@ -84,7 +91,7 @@ class TileGather:
     def __init__(self, renderer, width: int, height: int, *, group=None, row_block: int = 8, dst: int = 0,
                  out: str | None = None, slots: int = 2, native: bool | None = None,
                  persistent_frames: bool = False, loopback: bool = False, comm_reserve: int | None = None,
-                 rows: bool | None = None) -> None:
+                 rows: bool | None = None, shares: tuple | None = None) -> None:
         """``native``: drive each frame through rtx_tiles_submit (default: under RCCL with a
         renderer that has ``submit_tiles``); False keeps torch.distributed.gather. ``persistent_frames``
         (native root): assemble every frame of a slot into one buffer kept by the slot, so a frame
@@ -96,7 +103,10 @@ class TileGather:
         uint8 frames): every row block travels on its own straight into the root's frame
         (RTX_TILES_ROWS), with no assembly pass on the root. Off by default: RCCL charges ~2.7 us per
         operation (one GPU, C4 loopback: 5,480 us per step with row blocks of 8 rows, 2,837 with 32,
-        against 2,190 gathered whole and assembled)."""
+        against 2,190 gathered whole and assembled). ``shares`` = (root_run, run): rank 0 renders
+        root_run parts and every other rank run parts of a root_run + (world - 1) run interleave
+        (tiling.runs); default ROOT_SHARES by world size (the root also receives and assembles every
+        frame, so it takes a smaller share at 4 ranks and more; the root must then be rank 0)."""
         import torch.distributed as dist
 
         self._dist = dist
@@ -111,10 +121,17 @@ class TileGather:
         self.out = "u8" if out == "u8" else None
         dtype = torch.uint8 if self.out == "u8" else getattr(renderer, "color_dtype", torch.float64)
         self.device = torch.device(getattr(renderer, "device", "cpu"))
-        self.shape = tiling.tile_shape(self.H, self.W, self.rb, self.world, self.rank, self.out)
+        if shares is None:
+            shares = ROOT_SHARES.get(self.world, (1, 1)) if self.dst == 0 else (1, 1)
+        self.root_run, self.run = int(shares[0]), int(shares[1])
+        if self.root_run != self.run and self.dst != 0:
+            raise ValueError("unequal shares need the root at rank 0")
+        self.n_parts, runs = tiling.runs(self.world, self.root_run, self.run)
+        self.first, self.my_run = runs[self.rank]
+        self.shape = tiling.tile_shape(self.H, self.W, self.rb, self.n_parts, self.first, self.out, self.my_run)
         self.n = int(np.prod(self.shape))
         plen = tiling.part_len(self.H, self.W, self.rb, self.world, torch.empty((), dtype=dtype).element_size(),
-                               self.out)
+                               self.out, self.root_run, self.run)
         self._pending: dict = {}
         self.plan = None
         if native is None:
@@ -163,6 +180,7 @@ class TileGather:
         with torch.cuda.device(self.device):
             L.check(self._lib.rtx_tiles_create(comm, self.world, self.rank, self.dst, self.W, self.H, self.rb, kind,
                                                slots, send, recv, plen * torch.empty((), dtype=dtype).element_size(),
+                                               self.root_run, self.run,
                                                (L.TILES_LOOPBACK if loop else 0) | (L.TILES_ROWS if self.rows else 0)
                                                | ((reserve & 0xFFF) << L.F_RESERVE_SHIFT),
                                                ctypes.byref(plan)),
@@ -186,15 +204,16 @@ class TileGather:
             if self.rank == self.dst:
                 frame = (self.frames[slot] if self.frames is not None
                          else torch.empty(self.frame_shape, dtype=self._dtype, device=self.device))
-            self.r.submit_tiles(self.plan, slot, scene, self.rb, self.world, self.rank, frame)
+            self.r.submit_tiles(self.plan, slot, scene, self.rb, self.n_parts, self.first, frame, part_run=self.my_run)
             self._pending[slot] = (None, frame)
             return
         buf = self.send[slot]
         view = self._views[slot]
         if self._into:
-            self.r.render_tile(scene, self.rb, self.world, self.rank, self.out, into=view)
+            self.r.render_tile(scene, self.rb, self.n_parts, self.first, self.out, into=view, part_run=self.my_run)
         else:  # a renderer without into= (test stand-ins): copy its tile in
-            view.copy_(self.r.render_tile(scene, self.rb, self.world, self.rank, self.out))
+            kw = {"part_run": self.my_run} if self.my_run != 1 else {}
+            view.copy_(self.r.render_tile(scene, self.rb, self.n_parts, self.first, self.out, **kw))
         send = buf.cpu() if (self.gloo and buf.is_cuda) else buf
         gl = self._recv_lists[slot] if self.rank == self.dst else None
         work = self._dist.gather(send, gl, dst=self.dst, group=self.group, async_op=True)
@@ -215,8 +234,8 @@ class TileGather:
             return None
         tiles = self.recv[slot]
         if hasattr(self.r, "assemble_rows"):  # HipRenderer: the device un-permute
-            return self.r.assemble_rows(tiles, self.W, self.H, self.rb, self.out)
-        return tiling.assemble(tiles, self.H, self.W, self.rb, self.out)
+            return self.r.assemble_rows(tiles, self.W, self.H, self.rb, self.out, self.root_run, self.run)
+        return tiling.assemble(tiles, self.H, self.W, self.rb, self.out, self.root_run, self.run)
 
     def render(self, scene):
         """One frame, synchronous in program order: submit + finish on slot 0."""

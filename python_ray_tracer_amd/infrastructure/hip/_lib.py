@@ -83,6 +83,7 @@ EXPORTS = (
     "rtx_selftest_math",
     "rtx_assemble_rows",
     "rtx_shade_hits",
+    "rtx_assemble_runs",
     "rtx_sched_tiles",
     "rtx_render_camera_sched",
     "rtx_rccl_load",
@@ -132,11 +133,12 @@ _SIGS = {
     "rtx_comm_init": (_i32, [_c_void_p, _i32, _i32, _i32, ctypes.POINTER(_c_void_p)]),
     "rtx_comm_destroy": (_i32, [_c_void_p]),
     "rtx_tiles_create": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_c_void_p),
-                                ctypes.POINTER(_c_void_p), _i64, ctypes.c_uint, ctypes.POINTER(_c_void_p)]),
+                                ctypes.POINTER(_c_void_p), _i64, _i32, _i32, ctypes.c_uint, ctypes.POINTER(_c_void_p)]),
+    "rtx_assemble_runs": (_i32, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "rtx_tiles_submit": (_i32, [_c_void_p, _i32, _c_void_p, _i32, _i32, _c_void_p, _size, ctypes.c_uint, _c_void_p,
                                 _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "rtx_sched_tiles": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i64)]),
-    "rtx_render_camera_sched": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
+    "rtx_render_camera_sched": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _i32,
                                        _c_void_p, _size, _c_void_p, _c_void_p, ctypes.c_uint, _c_void_p, _c_void_p,
                                        _c_void_p]),
     "rtx_tiles_finish": (_i32, [_c_void_p, _i32, _c_void_p]),

@@ -336,17 +336,18 @@ class HipRenderer(Renderer):
     @_on_device
     def render_tile(self, scene, row_block: int = 1, n_parts: int = 1, part: int = 0, out: str | None = None,
                     blob: torch.Tensor | None = None, n_spheres: int | None = None,
-                    into: torch.Tensor | None = None) -> torch.Tensor:
+                    into: torch.Tensor | None = None, part_run: int = 1) -> torch.Tensor:
         """Render the interleaved row tile ``part`` of ``n_parts`` (row blocks of ``row_block``) of
         the scene camera's frame. Returns [3, rows*W] colour (``out=None``) or [rows, W, 3] uint8
         (``out="u8"``), rows in local order (python_ray_tracer_amd.tiling.tile_rows).
 
         ``into``: a contiguous device tensor of that shape and dtype to render into (a
         pre-allocated gather buffer) instead of a new one. ``blob``/``n_spheres``: an already
-        packed device scene (checked against its header)."""
+        packed device scene (checked against its header). ``part_run``: the run of parts
+        part .. part + part_run - 1 as one tile (tiling.tile_rows with run)."""
         W = int(scene.camera.width)
         blob, n_spheres, rows, ws, flags, probe, key, order, cost = self._tile_launch(scene, row_block, n_parts, part,
-                                                                                      blob, n_spheres)
+                                                                                      blob, n_spheres, part_run)
         n = W * rows
         if out == "u8":
             shape, dtype, kind = (rows, W, 3), torch.uint8, L.OUT_U8_HWC
@@ -361,7 +362,7 @@ class HipRenderer(Renderer):
                                  f"{into.dtype} {tuple(into.shape)} on {into.device}")
             res = into
         L.check(self._lib.rtx_render_camera_sched(blob.data_ptr(), n_spheres, W, int(scene.camera.height), row_block,
-                                                  n_parts, part, rows, self._bounces_arg, res.data_ptr(), kind,
+                                                  n_parts, part, part_run, rows, self._bounces_arg, res.data_ptr(), kind,
                                                   ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream(), flags,
                                                   _ptr(probe), _ptr(order), _ptr(cost)), "rtx_render_camera")
         self._after_launch(key, probe, cost)
@@ -374,7 +375,7 @@ class HipRenderer(Renderer):
         if cost is not None:
             self._cost_landed(key, cost)
 
-    def _tile_launch(self, scene, row_block, n_parts, part, blob=None, n_spheres=None):
+    def _tile_launch(self, scene, row_block, n_parts, part, blob=None, n_spheres=None, part_run=1):
         """What a camera launch of one row tile needs: (blob, n_spheres, local rows, workspace, flags,
         probe, key, tile order, tile cost) — the scene's device blob (cached by content, or the
         caller's, checked), the general-kernel plan of a capped render (_general_plan) and the
@@ -386,12 +387,12 @@ class HipRenderer(Renderer):
             blob, n_spheres = self._scene_entry(key)
         else:
             _check_blob(blob, n_spheres, self.device)
-        rows = n_local_rows(H, row_block, n_parts, part)
+        rows = n_local_rows(H, row_block, n_parts, part, part_run)
         ws = self.workspace(int(scene.camera.width) * rows)
         flags, probe, order, cost = 0, None, None, None
         capped = self.max_bounces is not None and self.max_bounces <= L.FAST_MAX_BOUNCES
         if key is not None and self.stats_buffer is None:
-            key = (key, row_block, n_parts, part, self.max_bounces)
+            key = (key, row_block, n_parts, part, part_run, self.max_bounces)
             if capped:
                 flags, probe = self._general_plan(key)
             if self.learn_tile_order:
@@ -423,11 +424,13 @@ class HipRenderer(Renderer):
         self._sched[key] = torch.argsort(cost, descending=True, stable=True).to(torch.int32)
 
     @_on_device
-    def submit_tiles(self, plan, slot: int, scene, row_block: int, n_parts: int, part: int, frame) -> None:
+    def submit_tiles(self, plan, slot: int, scene, row_block: int, n_parts: int, part: int, frame,
+                     part_run: int = 1) -> None:
         """One frame of a row-tiled plan (rtx_tiles_submit, distributed.TileGather): this rank's tile
         of ``scene`` rendered into the plan's slot, the RCCL gather to the root and, there, the
         assembly into ``frame`` (None on peers), all enqueued by one native call."""
-        blob, n_spheres, rows, ws, flags, probe, key, order, cost = self._tile_launch(scene, row_block, n_parts, part)
+        blob, n_spheres, rows, ws, flags, probe, key, order, cost = self._tile_launch(scene, row_block, n_parts, part,
+                                                                                      part_run=part_run)
         L.check(self._lib.rtx_tiles_submit(plan, int(slot), blob.data_ptr(), n_spheres, self._bounces_arg,
                                            ws.data_ptr(), ws.numel(), flags, _ptr(probe), _ptr(order), _ptr(cost),
                                            _ptr(frame), self._stream()), "rtx_tiles_submit")
@@ -595,11 +598,12 @@ class HipRenderer(Renderer):
 
     @_on_device
     def assemble_rows(self, tiles: torch.Tensor, width: int, height: int, row_block: int,
-                      out: str | None = None) -> torch.Tensor:
+                      out: str | None = None, root_run: int = 1, run: int = 1) -> torch.Tensor:
         """Frame from gathered row tiles (rtx_assemble_rows, the device un-permute of the
         multi-GPU path): ``tiles`` is [n_parts, part_len], part p holding render_tile(...,
         row_block, n_parts, p, out) flattened at its start. Returns what a whole-frame
-        render_tile returns: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``)."""
+        render_tile returns: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``). ``root_run`` /
+        ``run``: tile r is the run of parts of rank r (tiling.runs)."""
         P = int(tiles.shape[0])
         if tiles.device != self.device or not tiles.is_contiguous():
             tiles = tiles.to(self.device).contiguous()
@@ -609,8 +613,8 @@ class HipRenderer(Renderer):
             kind = _OUT_KIND[tiles.dtype]
             res = torch.empty((3, height * width), dtype=tiles.dtype, device=self.device)
         stride = tiles.stride(0) * tiles.element_size()
-        L.check(self._lib.rtx_assemble_rows(tiles.data_ptr(), stride, P, width, height, row_block, kind,
-                                            res.data_ptr(), self._stream()), "rtx_assemble_rows")
+        L.check(self._lib.rtx_assemble_runs(tiles.data_ptr(), stride, P, root_run, run, width, height, row_block, kind,
+                                            res.data_ptr(), self._stream()), "rtx_assemble_runs")
         return res
 
     def stats(self) -> dict:

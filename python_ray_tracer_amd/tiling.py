@@ -1,6 +1,8 @@
 """Interleaved row tiling of a frame across ranks (the multi-GPU split of SURVEY.md §8e).
 
-Rows are cut in blocks of ``row_block``; block b belongs to part ``b % n_parts``. Interleaving
+Rows are cut in blocks of ``row_block``; block b belongs to part ``b % n_parts``. A rank may render
+a run of consecutive parts (a larger or smaller share of the frame, ``runs``): part_run *
+row_block consecutive rows of every cycle. Interleaving
 balances the load: sky rows (no hit, ~15 flops/pixel) and ground rows (thousands) alternate
 across ranks instead of landing on one rank as contiguous strips would. Local row ``lr`` of part
 ``p`` is global row ``((lr // rb) * P + p) * rb + lr % rb`` — the mapping the kernel uses
@@ -18,52 +20,69 @@ from __future__ import annotations
 import numpy as np
 
 
-def n_local_rows(height: int, row_block: int, n_parts: int, part: int) -> int:
-    if row_block <= 0 or n_parts <= 0 or not 0 <= part < n_parts:
-        raise ValueError(f"bad tiling: row_block={row_block} n_parts={n_parts} part={part}")
-    cycle = row_block * n_parts
+def n_local_rows(height: int, row_block: int, n_parts: int, part: int, run: int = 1) -> int:
+    """Rows of the run of ``run`` consecutive parts from ``part``: run * row_block rows of every
+    cycle of n_parts * row_block rows (the last cycle's prefix)."""
+    if row_block <= 0 or n_parts <= 0 or run <= 0 or not 0 <= part <= n_parts - run:
+        raise ValueError(f"bad tiling: row_block={row_block} n_parts={n_parts} part={part} run={run}")
+    cycle, own = row_block * n_parts, row_block * run
     q, rem = divmod(int(height), cycle)
-    return q * row_block + min(max(rem - part * row_block, 0), row_block)
+    return q * own + min(max(rem - part * row_block, 0), own)
 
 
-def tile_rows(height: int, row_block: int, n_parts: int, part: int) -> np.ndarray:
-    """Global row index of each local row of ``part`` (ascending)."""
-    n = n_local_rows(height, row_block, n_parts, part)
+def tile_rows(height: int, row_block: int, n_parts: int, part: int, run: int = 1) -> np.ndarray:
+    """Global row index of each local row of the run of ``run`` parts from ``part`` (ascending)."""
+    n = n_local_rows(height, row_block, n_parts, part, run)
     lr = np.arange(n)
-    return ((lr // row_block) * n_parts + part) * row_block + lr % row_block
+    own = row_block * run
+    return (lr // own) * (n_parts * row_block) + part * row_block + lr % own
+
+
+def runs(world: int, root_run: int = 1, run: int = 1):
+    """(n_parts, [(first part, run) per rank]) of the shares: rank 0 renders parts [0, root_run),
+    rank i >= 1 parts [root_run + (i - 1) run, root_run + i run)."""
+    n_parts = root_run + (world - 1) * run
+    return n_parts, [(0, root_run)] + [(root_run + (i - 1) * run, run) for i in range(1, world)]
 
 
 def max_local_rows(height: int, row_block: int, n_parts: int) -> int:
     return n_local_rows(height, row_block, n_parts, 0)  # part 0 has the most rows
 
 
-def tile_shape(height: int, width: int, row_block: int, n_parts: int, part: int, out: str | None = None):
-    """Shape ``render_tile`` returns for this part: (3, rows*W) colour or (rows, W, 3) uint8."""
-    rows = n_local_rows(height, row_block, n_parts, part)
+def tile_shape(height: int, width: int, row_block: int, n_parts: int, part: int, out: str | None = None,
+               run: int = 1):
+    """Shape ``render_tile`` returns for this part (or run of parts): (3, rows*W) colour or
+    (rows, W, 3) uint8."""
+    rows = n_local_rows(height, row_block, n_parts, part, run)
     return (rows, int(width), 3) if out == "u8" else (3, rows * int(width))
 
 
-def part_len(height: int, width: int, row_block: int, n_parts: int, itemsize: int, out: str | None = None) -> int:
-    """Elements of one gather buffer: the largest part's tile, rounded up to 16 bytes (so every
-    part of a [n_parts, part_len] buffer starts 16-byte aligned for the device copy)."""
-    n = 3 * max_local_rows(height, row_block, n_parts) * int(width)
+def part_len(height: int, width: int, row_block: int, n_parts: int, itemsize: int, out: str | None = None,
+             root_run: int = 1, run: int = 1) -> int:
+    """Elements of one gather buffer: the largest rank's tile (``n_parts`` ranks, shares as in
+    ``runs``), rounded up to 16 bytes (so every tile of a [ranks, part_len] buffer starts 16-byte
+    aligned for the device copy)."""
+    np_, shares = runs(n_parts, root_run, run)
+    n = 3 * max(n_local_rows(height, row_block, np_, f, k) for f, k in shares) * int(width)
     per16 = max(1, 16 // itemsize)
     return (n + per16 - 1) // per16 * per16
 
 
-def assemble(tiles, height: int, width: int, row_block: int, out: str | None = None):
-    """Un-permute gathered part buffers ``tiles[p]`` (each ``part_len`` long, layout above) into
-    one frame: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``). Torch tensors or NumPy arrays."""
+def assemble(tiles, height: int, width: int, row_block: int, out: str | None = None, root_run: int = 1,
+             run: int = 1):
+    """Un-permute gathered rank buffers ``tiles[r]`` (each ``part_len`` long, layout above; shares
+    as in ``runs``) into one frame: [3, H*W] colour or [H, W, 3] uint8 (``out="u8"``). Torch tensors
+    or NumPy arrays."""
     import torch
 
-    n_parts = len(tiles)
+    n_parts, shares = runs(len(tiles), root_run, run)
     first = tiles[0]
     is_torch = isinstance(first, torch.Tensor)
     shape = (height, width, 3) if out == "u8" else (3, height, width)
     full = (torch.empty(shape, dtype=first.dtype, device=first.device) if is_torch
             else np.empty(shape, dtype=first.dtype))
-    for p in range(n_parts):
-        rows = tile_rows(height, row_block, n_parts, p)
+    for p, (f, k_run) in enumerate(shares):
+        rows = tile_rows(height, row_block, n_parts, f, k_run)
         k = len(rows)
         if k == 0:
             continue

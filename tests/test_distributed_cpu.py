@@ -26,10 +26,10 @@ class OracleTileRenderer:
     def __init__(self, B):
         self.B = B
 
-    def render_tile(self, scene, row_block, n_parts, part, out=None):
+    def render_tile(self, scene, row_block, n_parts, part, out=None, part_run=1):
         sc = O.scene_from_objects(scene)
         W, H = sc.width, sc.height
-        rows = tiling.tile_rows(H, row_block, n_parts, part)
+        rows = tiling.tile_rows(H, row_block, n_parts, part, part_run)
         full = O.render(sc, self.B).reshape(3, H, W)
         t = full[:, rows].reshape(3, -1)
         if out == "u8":
@@ -90,8 +90,9 @@ def _worker(rank, world, port, spec, B, row_block, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,row_block", [(2, 8), (3, 4)])
+@pytest.mark.parametrize("world,row_block", [(2, 8), (3, 4), (4, 4)])
 def test_row_tiles_gather_equals_single_frame(world, row_block):
+    """world 4: the default shares give the root one part and the peers two each (ROOT_SHARES)."""
     spec = scenes.readme_spec(40, 27)  # 27 rows: uneven split, padding exercised
     B = 3
     with tempfile.TemporaryDirectory() as d:

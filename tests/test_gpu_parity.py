@@ -185,6 +185,32 @@ def test_row_tiles_reassemble(hip):
     assert torch.equal(r.render_tile(scene, blob=blob, n_spheres=S), full)
 
 
+def test_row_tile_shares_reassemble(hip):
+    """Weighted shares (distributed.ROOT_SHARES): the root renders root_run parts and every other
+    rank run parts of the root_run + (world-1)*run interleave, each share one render_tile(...,
+    part_run=) launch; the device un-permute (rtx_assemble_runs) and the host one give the
+    single-GPU frame bit for bit."""
+    from python_ray_tracer_amd import tiling
+
+    spec = scenes.readme_spec(200, 117)
+    scene = scenes.build_scene(spec)
+    r = hip.HipRenderer(max_bounces=3, color_dtype=torch.float32)
+    full = r.render(scene).data
+    full_u8 = r.quantize(r.render(scene), scene.camera)
+    for world, root_run, run, rb in ((4, 1, 2, 8), (8, 1, 2, 8), (3, 2, 3, 5), (5, 1, 3, 1)):
+        n_parts, shares = tiling.runs(world, root_run, run)
+        for out, ref, isz in ((None, full, full.element_size()), ("u8", full_u8, 1)):
+            n = tiling.part_len(117, 200, rb, world, isz, out, root_run, run)
+            buf = torch.full((world, n), 7, dtype=ref.dtype, device=ref.device)
+            for k, (first, k_run) in enumerate(shares):
+                shp = tiling.tile_shape(117, 200, rb, n_parts, first, out, k_run)
+                view = buf[k, :int(np.prod(shp))].view(shp)
+                r.render_tile(scene, rb, n_parts, first, out=out, into=view, part_run=k_run)
+            case = (world, root_run, run, rb, out)
+            assert torch.equal(r.assemble_rows(buf, 200, 117, rb, out, root_run, run), ref), case
+            assert torch.equal(tiling.assemble(buf.cpu(), 117, 200, rb, out, root_run, run), ref.cpu()), case
+
+
 def test_render_batch_matches_single_frames(hip):
     """rtx_render_frames: an orbit animation (C5 camera path) and a batch of different scenes in
     ONE launch equal one render per frame bit for bit, on the fast kernel (B=3) and beyond its cap

@@ -108,17 +108,22 @@ def test_sched_and_tiles_entry_points_validate_on_host():
     assert lib.rtx_sched_tiles(3840, 2160, 17, ctypes.byref(n)) == 0 and n.value == 120 * 270
     assert lib.rtx_sched_tiles(1920, 0, 3, ctypes.byref(n)) == 0 and n.value == 0
     # unknown flag bits are refused before anything is launched
-    rc = lib.rtx_render_camera_sched(None, 3, 16, 16, 1, 1, 0, 16, 3, None, 0, None, 0, None, None, 1 << 20, None,
+    rc = lib.rtx_render_camera_sched(None, 3, 16, 16, 1, 1, 0, 1, 16, 3, None, 0, None, 0, None, None, 1 << 20, None,
                                      None, None)
     assert rc == -1 and b"flags" in lib.rtx_last_error()
     plan = ctypes.c_void_p()
     ptrs = (ctypes.c_void_p * 2)(1, 1)
     # a gathering plan needs a communicator (RTX_E_COMM); RTX_TILES_ROWS needs uint8 frames
-    assert lib.rtx_tiles_create(None, 2, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, ptrs, ptrs, 4096, 0, ctypes.byref(plan)) == -4
-    assert lib.rtx_tiles_create(None, 2, 0, 0, 64, 64, 8, L.OUT_F32_SOA, 2, ptrs, ptrs, 8192, L.TILES_ROWS,
+    assert lib.rtx_tiles_create(None, 2, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, ptrs, ptrs, 4096, 1, 1, 0,
+                                ctypes.byref(plan)) == -4
+    assert lib.rtx_tiles_create(None, 2, 0, 0, 64, 64, 8, L.OUT_F32_SOA, 2, ptrs, ptrs, 8192, 1, 1, L.TILES_ROWS,
                                 ctypes.byref(plan)) == -1
-    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 9, None, None, 16, 0, ctypes.byref(plan)) == -1
-    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, None, None, 16, 1 << 20,
+    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 9, None, None, 16, 1, 1, 0,
+                                ctypes.byref(plan)) == -1
+    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, None, None, 16, 1, 1, 1 << 20,
+                                ctypes.byref(plan)) == -1
+    # unequal shares: rank 0 must be the root, and a one-rank plan has one share
+    assert lib.rtx_tiles_create(None, 1, 0, 0, 64, 64, 8, L.OUT_U8_HWC, 2, None, None, 16, 1, 2, 0,
                                 ctypes.byref(plan)) == -1
     assert plan.value is None
     assert lib.rtx_tiles_submit(None, 0, None, 3, 3, None, 0, 0, None, None, None, None, None) == -1
