@@ -279,7 +279,8 @@ int rtx_render_camera_ex(const double* scene, int n_spheres, int width, int heig
  *    would otherwise run alone at its end. Output does not depend on the order.
  *  - tile_cost (may be NULL; zero-filled): receives each unit's render time (s_memrealtime ticks,
  *    100 MHz; a block tile: its slowest wave) in this launch, from which a caller derives the order
- *    of the next identical launch. */
+ *    of the next identical launch. A recording launch runs the kernel build that carries the
+ *    counters (slower; the records stay out of the timed build's registers), so record once. */
 int rtx_sched_tiles(int width, int n_local_rows, int n_spheres, int64_t* n_tiles);
 int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int height,
                             int row_block, int n_parts, int part, int part_run, int n_local_rows,

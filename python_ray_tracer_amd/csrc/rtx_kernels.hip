@@ -146,7 +146,7 @@ struct Params {
              // 3: explicit rays whose level-0 hit is given (hit_shape at hit_t: Shader.create)
   // camera mode: local rows of parts part .. part + part_run - 1 of the n_parts-way row interleave
   int width, height, row_block, n_parts, part, n_rows;
-  int part_run;
+  int part_run = 1;
   // explicit-ray mode
   const double* org;
   int64_t org_stride;
@@ -1902,7 +1902,6 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
   // -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%)
   constexpr bool BEAM = TP >= 2 && !DEEP;
   extern __shared__ double lds_tab[];
-  const uint64_t t_entry = p0.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;  // (learning the dispatch order)
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
     // a blob that is not a packed scene of p.nsph spheres (the LDS table and every sphere loop are
@@ -1958,9 +1957,12 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     while (k < tiles_c) {
       const int t = order ? (int)order[c + k * nc] : c + k * nc;
       const int row = t / p.n_tiles_x;
-      const uint64_t tc0 = p.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;
+      // the tile's time as -start + end in its cost word. Cost records are kept to the STATS
+      // instantiations (run_render picks one for a launch that records them): in the timed kernel
+      // the record costs C4 six more spilled VGPRs and 2.5% (A/B r4h)
+      if (STATS && p.tile_cost && lane == 0) p.tile_cost[t] = 0u - (uint32_t)__builtin_amdgcn_s_memrealtime();
       fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
-      if (p.tile_cost && lane == 0) p.tile_cost[t] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc0);
+      if (STATS && p.tile_cost && lane == 0) atomicAdd(p.tile_cost + t, (uint32_t)__builtin_amdgcn_s_memrealtime());
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
       if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
@@ -1976,6 +1978,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
   // the order. Blocks are dispatched in blockIdx order: a host order (camera launches,
   // rtx_render_camera_sched) maps dispatch slot b to block tile order[b], block tile t being
   // (t % gridDim.x, bottom-up row t / gridDim.x), and a cost record takes each block's time.
+  const uint64_t t_entry = STATS && p.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;  // (learning the order)
   int bx = blockIdx.x, by = gridDim.y - 1 - blockIdx.y, tb = blockIdx.y * gridDim.x + blockIdx.x;
   if (p.tile_order) {
     tb = (int)((const uint32_t __attribute__((address_space(4)))*)p.tile_order)[tb];
@@ -1983,7 +1986,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     by = gridDim.y - 1 - tb / gridDim.x;
   }
   fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, bx, by, true, lds_tab);
-  if (p.tile_cost && (threadIdx.x & 63) == 0)  // the block's time: the slowest of its waves
+  if (STATS && p.tile_cost && (threadIdx.x & 63) == 0)  // the block's time: the slowest of its waves
     atomicMax(p.tile_cost + tb, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_entry));
 }
 
@@ -2476,7 +2479,8 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
   return dim3((unsigned)blocks);
 }
 
-// STATS: the instantiation with the per-level and executed-work counters (stats buffer given).
+// STATS: the instantiation with the per-level and executed-work counters (stats buffer given) and
+// the per-unit cost records (tile_cost given; counters only where p.stats is set).
 // Launches that are not persistent run instantiations without the persistent tile loop (TP 1), and
 // scenes below kTreeMinSpheres, which carry no culling tree (scene_pack.BVH_MIN_SPHERES), ones
 // without the tree walks either (TP 0) (A/B in DESIGN.md §4).
@@ -2501,7 +2505,7 @@ void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
 }
 template <int B, bool DEEP, bool LVL>
 void launch_fast_lds(Params& p, dim3 grid, hipStream_t s) {
-  if (p.stats) {
+  if (p.stats || p.tile_cost) {  // (the cost records of a learning launch live in the STATS kernels)
     launch_fast_lds_s<B, DEEP, LVL, true>(p, grid, s);
   } else {
     launch_fast_lds_s<B, DEEP, LVL, false>(p, grid, s);
@@ -2530,7 +2534,7 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
       }
     }
   } else {
-    if (p.stats) {
+    if (p.stats || p.tile_cost) {
       if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, false, DEEP, false, true>, 0, p);
       hipExtLaunchKernelGGL((k_render_fast<B, false, DEEP, false, true>), grid, dim3(kFastBlock), 0u, s,
                             prof_event(0), prof_event(1), 0u, p);
@@ -2747,8 +2751,9 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
                             void* workspace,
                             size_t workspace_bytes, uint64_t* stats, void* stream, unsigned flags,
                             uint32_t* deferred_out, const uint32_t* tile_order, uint32_t* tile_cost) {
-  if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
-      n_local_rows < 0 || n_local_rows > height)
+  if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part_run < 1 ||
+      part_run > n_parts - part || n_local_rows < 0 ||
+      n_local_rows > tile_local_rows(height, row_block, n_parts, part, part_run))
     return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
   if (flags & ~(unsigned)(RTX_F_NO_GENERAL | RTX_F_RESERVE(0xFFF)))
     return fail(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
@@ -2761,6 +2766,7 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
   p.row_block = row_block;
   p.n_parts = n_parts;
   p.part = part;
+  p.part_run = part_run;
   p.n_rows = n_local_rows;
   p.n = (int64_t)width * n_local_rows;
   p.max_bounces = max_bounces;
@@ -2855,7 +2861,7 @@ int rtx_ray_directions(const double* scene, int width, int height, int row_block
                        int n_local_rows, double* dirs_out, void* stream) {
   if (!scene || !dirs_out) return fail(RTX_E_ARG, "null pointer argument%s", "");
   if (width <= 0 || height <= 0 || row_block <= 0 || n_parts <= 0 || part < 0 || part >= n_parts ||
-      n_local_rows < 0 || n_local_rows > height)
+      n_local_rows < 0 || n_local_rows > tile_local_rows(height, row_block, n_parts, part))
     return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
   Params p{};
   p.scene = scene;

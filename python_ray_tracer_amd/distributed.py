@@ -41,10 +41,12 @@ COMM_RESERVE_BLOCKS = 64
 
 
 # Shares (root_run, run) of the row-tiled frame by world size: the root also receives every part and
-# assembles the frame beside its next render, so from 4 ranks on it renders one part where every
-# other rank renders two (the root's share that balances its render plus that traffic
-# against a peer's render is ~6-8% of the frame at 8 ranks, 1/15 here).
-ROOT_SHARES = {4: (1, 2), 5: (1, 2), 6: (1, 2), 7: (1, 2), 8: (1, 2)}
+# assembles the frame beside its next render (~0.33 us of render time per MB of that HBM traffic,
+# DESIGN.md §6), so it renders fewer rows than a peer. Chosen on the C4 part emulation (one GPU,
+# profiles/r4_shares_C4.json: slowest of root render + its traffic and a peer's render): 2 ranks
+# 8:9 (1,086 us against 1,145 equal), 4 ranks 3:4 (558 against 639), 8 ranks 1:2 (296 against 396);
+# 3, 5, 6 and 7 ranks interpolated, not measured.
+ROOT_SHARES = {2: (8, 9), 3: (3, 4), 4: (3, 4), 5: (2, 3), 6: (2, 3), 7: (1, 2), 8: (1, 2)}
 
 
 # RCCL communicators of the native path, one per (process group, rank, device): creating one costs
@@ -106,7 +108,7 @@ class TileGather:
         against 2,190 gathered whole and assembled). ``shares`` = (root_run, run): rank 0 renders
         root_run parts and every other rank run parts of a root_run + (world - 1) run interleave
         (tiling.runs); default ROOT_SHARES by world size (the root also receives and assembles every
-        frame, so it takes a smaller share at 4 ranks and more; the root must then be rank 0)."""
+        frame, so it takes a smaller share; the root must then be rank 0)."""
         import torch.distributed as dist
 
         self._dist = dist

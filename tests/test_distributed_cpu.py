@@ -92,7 +92,8 @@ def _worker(rank, world, port, spec, B, row_block, outdir):
 
 @pytest.mark.parametrize("world,row_block", [(2, 8), (3, 4), (4, 4)])
 def test_row_tiles_gather_equals_single_frame(world, row_block):
-    """world 4: the default shares give the root one part and the peers two each (ROOT_SHARES)."""
+    """The default shares (ROOT_SHARES): the root renders fewer row blocks than a peer; on this
+    27-row frame world 2 leaves the peer no rows and world 3 the last rank none (empty tiles)."""
     spec = scenes.readme_spec(40, 27)  # 27 rows: uneven split, padding exercised
     B = 3
     with tempfile.TemporaryDirectory() as d:

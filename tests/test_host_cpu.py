@@ -111,6 +111,11 @@ def test_sched_and_tiles_entry_points_validate_on_host():
     rc = lib.rtx_render_camera_sched(None, 3, 16, 16, 1, 1, 0, 1, 16, 3, None, 0, None, 0, None, None, 1 << 20, None,
                                      None, None)
     assert rc == -1 and b"flags" in lib.rtx_last_error()
+    # a run of parts past the interleave, an empty run, more local rows than the run owns
+    for part, run, rows in ((3, 2, 4), (0, 0, 4), (1, 2, 9)):
+        rc = lib.rtx_render_camera_sched(None, 3, 16, 16, 2, 4, part, run, rows, 3, None, 0, None, 0, None, None, 0,
+                                         None, None, None)
+        assert rc == -1 and b"geometry" in lib.rtx_last_error(), (part, run, rows)
     plan = ctypes.c_void_p()
     ptrs = (ctypes.c_void_p * 2)(1, 1)
     # a gathering plan needs a communicator (RTX_E_COMM); RTX_TILES_ROWS needs uint8 frames

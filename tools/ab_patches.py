@@ -303,8 +303,25 @@ __device__ __forceinline__ void trace_rec(const Params& p, unsigned long long t0
                 "int rtx_trace_set(void* buf) {\n  g_trace = (unsigned long long*)buf;\n  return RTX_OK;\n}\n")
 
 
+def persist_plain(src: str) -> str:
+    """The persistent loop (TP 2) without the learnt order and the per-tile cost records: the fixed
+    c + k * n_fetch tiles, no timestamps live across the tile."""
+    src = _sub(src, "const int t = order ? (int)order[c + k * nc] : c + k * nc;", "const int t = c + k * nc;")
+    src = _sub(src, "const uint64_t tc0 = p.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;\n", "")
+    return _sub(src, "if (p.tile_cost && lane == 0) p.tile_cost[t] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc0);\n",
+                "")
+
+
+def block_plain(src: str) -> str:
+    """One-tile-per-block launches (TP 0, 1) without the learnt order and the cost records."""
+    src = _sub(src, "const uint64_t t_entry = p0.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;", "")
+    src = _sub(src, "  if (p.tile_order) {\n    tb =", "  if (false) {\n    tb =")
+    return _sub(src, "  if (p.tile_cost && (threadIdx.x & 63) == 0)  // the block's time: the slowest of its waves\n"
+                "    atomicMax(p.tile_cost + tb, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_entry));\n", "")
+
+
 PATCHES = {f.__name__: f for f in (inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
-                                   lv_together, self_triple, lv_triple, tile_trace)}
+                                   lv_together, self_triple, lv_triple, tile_trace, persist_plain, block_plain)}
 
 
 def apply(src: str, names: str) -> str:
