@@ -241,7 +241,7 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
     rows_max = n > rows_max ? n : rows_max;
   }
   if (part_bytes < rows_max * (int64_t)width * bytes_per_pixel(out_kind) || part_bytes % 16 != 0)
-    return err(RTX_E_ARG, "part_bytes must hold part 0's tile and be a multiple of 16%s (%lld)", "", part_bytes);
+    return err(RTX_E_ARG, "part_bytes must hold the longest share's tile and be a multiple of 16%s (%lld)", "", part_bytes);
   for (int s = 0; s < slots; ++s) {
     if (rank == root && (world > 1 || loop) && (!recv || !recv[s]))
       return err(RTX_E_ARG, "the root needs a receive buffer per slot%s", "");

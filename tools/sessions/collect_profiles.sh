@@ -2,7 +2,7 @@
 # Copy one gpu_profile.sh session's results into profiles/ (tracked): bench lines, rocprofv3
 # kernel-stats CSVs and the timed-region summaries. Usage: bash tools/sessions/collect_profiles.sh <tag> <round-prefix>
 set -eu
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 TAG=$1; PFX=$2
 SRC=gpurun_out/$TAG
 for f in "$SRC"/bench_*.json; do
