@@ -251,6 +251,11 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
  *    flag (the workspace counters stay clean, so later calls are unaffected). Uncapped renders
  *    ignore it. */
 #define RTX_F_NO_GENERAL 1u
+/* RTX_F_IMAGES: the scene has image-textured spheres (RTX_TEX_IMAGE). A capped render then runs the
+ * fast kernel's texturing build, which shades those hits itself (the texel lookup compiled in);
+ * without the flag they are deferred to k_render_general like ties (same colours either way; the
+ * texturing build costs untextured scenes 3-7%, so it is opt-in). Uncapped renders ignore it. */
+#define RTX_F_IMAGES 2u
 /* RTX_F_RESERVE(n): a persistent launch (>= 32 spheres, one frame) sizes its grid n blocks below what
  * the device holds at once, leaving room for the kernels of a collective running beside it (the
  * row-tiled frame's RCCL gather of the previous frame: the persistent waves would otherwise hold

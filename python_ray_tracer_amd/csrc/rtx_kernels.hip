@@ -189,6 +189,7 @@ struct Params {
   int frame;  // set per block / per deferred ray (kernel side)
   uint32_t* deferred_out;  // the launch's deferred-ray count (rtx_render_camera_ex), or null
   int no_general;  // RTX_F_NO_GENERAL: no general kernel follows, so nothing may be deferred
+  int images;      // RTX_F_IMAGES: the capped LDS kernels shade image-textured spheres themselves
   // camera launches of one frame (rtx_render_camera_sched): the dispatch units (the persistent
   // launch's wave tiles, else the grid's block tiles) in dispatch order (null: bottom-up row order),
   // and per-unit render times to record (s_memrealtime ticks), or null
@@ -1571,7 +1572,9 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // overlaps the LDS staging of the scene table. DEEP (caps above 8 or none): chains still alive
 // after B levels are deferred with a resume record, and the continuation mode exists; the capped
 // instantiations compile none of it.
-template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM>
+// IMG: image-textured spheres are shaded here (the texel lookup compiled in, RTX_F_IMAGES launches)
+// instead of deferred to the general kernel.
+template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM, bool IMG = false>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   constexpr int FB = fast_block<TREE>();  // threads per block of this instantiation
@@ -1712,9 +1715,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     Hit s;
     if constexpr (LDS) {
-      shade<false, TREE>(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
+      shade<IMG, TREE>(sc, geo, (const double*)lds_tab, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
     } else {
-      shade<false, TREE>(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
+      shade<IMG, TREE>(sc, geo, p.scene + RTX_HDR_WORDS, nsph, hit, ox, oy, oz, dx, dy, dz, tmin, s, tame, wk);
     }
     if (s.tk < 0) {  // an image-textured sphere: so is this one (the texel lookup stays out of here)
       deferred = true;
@@ -1765,7 +1768,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (!weighted || k >= B || at_cap) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
       const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
-      hit_color(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
+      hit_color<IMG>(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
                 s.va, 0.0, 0.0, 0.0, cr, cg, cb);
       break;
     }
@@ -1853,7 +1856,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if constexpr (NL < B) {
       for (int d = depth - 1; d >= NL; --d) {  // the register levels first (the deepest)
         const int key = sKey[0];
-        hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], key_tex(key), true, true,
+        hit_color<IMG>(mtab + key_hit(key) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], key_tex(key), true, true,
                   sSpec[0], sVa[0], cr, cg, cb, cr, cg, cb);
 #pragma unroll
         for (int j = 0; j < NR - 1; ++j) {
@@ -1865,13 +1868,13 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     for (int d = (depth < NL ? depth : NL) - 1; d >= 0; --d) {
       const double* const l = lvd + (d * 4) * FB + lt;
       const int key = lvk[d * FB + lt];
-      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, l[0], l[FB], key_tex(key), true, true,
+      hit_color<IMG>(mtab + key_hit(key) * RTX_MAT_WORDS, sc, l[0], l[FB], key_tex(key), true, true,
                 l[2 * FB], l[3 * FB], cr, cg, cb, cr, cg, cb);
     }
   } else {
     for (int d = 0; d < depth; ++d) {
       const int key = sKey[0];
-      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], key_tex(key), true, true, sSpec[0],
+      hit_color<IMG>(mtab + key_hit(key) * RTX_MAT_WORDS, sc, sDli[0], sDi[0], key_tex(key), true, true, sSpec[0],
                 sVa[0], cr, cg, cb, cr, cg, cb);
 #pragma unroll
       for (int j = 0; j < NS - 1; ++j) {
@@ -1884,7 +1887,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     for (int l = kb - 1; l >= 0; --l) {
       const double* lv = rin + 6 + kRecLevelWords * l;
       const int key = (int)lv[4];
-      hit_color(mtab + key_hit(key) * RTX_MAT_WORDS, sc, lv[0], lv[1], key_tex(key), true, true, lv[2], lv[3],
+      hit_color<IMG>(mtab + key_hit(key) * RTX_MAT_WORDS, sc, lv[0], lv[1], key_tex(key), true, true, lv[2], lv[3],
                 cr, cg, cb, cr, cg, cb);
     }
   }
@@ -1893,7 +1896,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 
 // TP: 0 = no culling tree and no persistent launch (scenes below kTreeMinSpheres), 1 = culling tree,
 // one tile per block (the launch is not persistent), 2 = both (persistent launches)
-template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2>
+template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2,
+          bool IMG = false>
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
                              (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
                                                       : kFastWavesPerSimd)) void k_render_fast(Params p0) {
@@ -1922,7 +1926,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
       for (int64_t t = blockIdx.x; t * fast_block<TREE>() < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
     }
@@ -1961,7 +1965,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
       // instantiations (run_render picks one for a launch that records them): in the timed kernel
       // the record costs C4 six more spilled VGPRs and 2.5% (A/B r4h)
       if (STATS && p.tile_cost && lane == 0) p.tile_cost[t] = 0u - (uint32_t)__builtin_amdgcn_s_memrealtime();
-      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
+      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
       if (STATS && p.tile_cost && lane == 0) atomicAdd(p.tile_cost + t, (uint32_t)__builtin_amdgcn_s_memrealtime());
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
@@ -1985,7 +1989,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     bx = tb % gridDim.x;
     by = gridDim.y - 1 - tb / gridDim.x;
   }
-  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM>(p, bx, by, true, lds_tab);
+  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, bx, by, true, lds_tab);
   if (STATS && p.tile_cost && (threadIdx.x & 63) == 0)  // the block's time: the slowest of its waves
     atomicMax(p.tile_cost + tb, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_entry));
 }
@@ -2313,7 +2317,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble_rows(const uint8_t* __restr
 // Launches k_render_fast<B, true, deep, lvl, stats, 0>(*params) on s (events e0/e1 as
 // hipExtLaunchKernelGGL's); hipErrorInvalidValue, nothing launched, for an instantiation the unit
 // does not carry.
-__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats,
+__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats, bool img,
                                                                   const void* params, dim3 grid, uint32_t lds,
                                                                   hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 namespace {
@@ -2484,29 +2488,32 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
 // Launches that are not persistent run instantiations without the persistent tile loop (TP 1), and
 // scenes below kTreeMinSpheres, which carry no culling tree (scene_pack.BVH_MIN_SPHERES), ones
 // without the tree walks either (TP 0) (A/B in DESIGN.md §4).
-template <int B, bool DEEP, bool LVL, bool STATS>
+template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   const bool small = p.nsph < kTreeMinSpheres;  // the TREE = false kernels: fast_block<false>() threads
   const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
                      (LVL ? (small ? level_lds_bytes<DEEP, false>(B) : level_lds_bytes<DEEP>(B)) : 0);
   if (p.n_fetch == 0) {  // one tile per block: the instantiations without the persistent loop
     if (p.nsph < kTreeMinSpheres) {  // TP 0: the rtx_small.hip unit
-      const hipError_t e = rtx_launch_small(B, DEEP, LVL, STATS, &p, grid, (uint32_t)lds, s, prof_event(0), prof_event(1));
+      const hipError_t e =
+          rtx_launch_small(B, DEEP, LVL, STATS, IMG, &p, grid, (uint32_t)lds, s, prof_event(0), prof_event(1));
       if (e != hipSuccess) g_small_err = e;
     } else {
-      hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 1>), grid, dim3(kFastBlock), (uint32_t)lds, s,
-                            prof_event(0), prof_event(1), 0u, p);
+      hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 1, IMG>), grid, dim3(kFastBlock), (uint32_t)lds,
+                            s, prof_event(0), prof_event(1), 0u, p);
     }
     return;
   }
-  if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL, STATS>, lds, p);
-  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS>), grid, dim3(kFastBlock), (uint32_t)lds, s,
+  if (p.n_fetch > 0) grid = persistent_grid(k_render_fast<B, true, DEEP, LVL, STATS, 2, IMG>, lds, p);
+  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 2, IMG>), grid, dim3(kFastBlock), (uint32_t)lds, s,
                         prof_event(0), prof_event(1), 0u, p);
 }
 template <int B, bool DEEP, bool LVL>
 void launch_fast_lds(Params& p, dim3 grid, hipStream_t s) {
   if (p.stats || p.tile_cost) {  // (the cost records of a learning launch live in the STATS kernels)
     launch_fast_lds_s<B, DEEP, LVL, true>(p, grid, s);
+  } else if (!DEEP && p.images) {  // image textures shaded in place (capped renders only)
+    launch_fast_lds_s<B, DEEP, LVL, false, !DEEP>(p, grid, s);
   } else {
     launch_fast_lds_s<B, DEEP, LVL, false>(p, grid, s);
   }
@@ -2755,9 +2762,10 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
       part_run > n_parts - part || n_local_rows < 0 ||
       n_local_rows > tile_local_rows(height, row_block, n_parts, part, part_run))
     return fail(RTX_E_ARG, "bad frame/tile geometry%s", "");
-  if (flags & ~(unsigned)(RTX_F_NO_GENERAL | RTX_F_RESERVE(0xFFF)))
+  if (flags & ~(unsigned)(RTX_F_NO_GENERAL | RTX_F_IMAGES | RTX_F_RESERVE(0xFFF)))
     return fail(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
   Params p{};
+  p.images = (flags & RTX_F_IMAGES) ? 1 : 0;
   p.scene = scene;
   p.nsph = n_spheres;
   p.mode = 0;

@@ -8,11 +8,11 @@
 
 namespace {
 
-template <int B, bool DEEP, bool LVL, bool STATS>
+template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false>
 hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const Params& p = *static_cast<const Params*>(params);
-  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0>), grid, dim3(fast_block<false>()), lds, s, e0, e1,
-                        0u, p);
+  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0, IMG>), grid, dim3(fast_block<false>()), lds, s, e0,
+                        e1, 0u, p);
   return hipSuccess;  // launch errors reach the caller's check_launch through hipGetLastError
 }
 
@@ -20,29 +20,33 @@ hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEve
 // table always fits the LDS beside the level slots (levels_in_lds), DEEP keeps every level in LDS
 // (S <= kDeepLvMaxSpheres)
 template <int B, bool DEEP>
-hipError_t go_b(bool lvl, bool stats, const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0,
-                hipEvent_t e1) {
+hipError_t go_b(bool lvl, bool stats, bool img, const void* params, dim3 grid, uint32_t lds, hipStream_t s,
+                hipEvent_t e0, hipEvent_t e1) {
   constexpr bool kLvl = DEEP ? kLevelsInLds : levels_in_lds<B, true, false>();
   static_assert(!DEEP || kDeepLvMaxSpheres >= kTreeMinSpheres, "small DEEP scenes keep their levels in LDS");
   if (lvl != kLvl) return hipErrorInvalidValue;
+  if (img) {  // image textures shaded in place: capped, counter-free launches only
+    if constexpr (DEEP) return hipErrorInvalidValue;
+    else return stats ? hipErrorInvalidValue : go<B, DEEP, kLvl, false, true>(params, grid, lds, s, e0, e1);
+  }
   return stats ? go<B, DEEP, kLvl, true>(params, grid, lds, s, e0, e1)
                : go<B, DEEP, kLvl, false>(params, grid, lds, s, e0, e1);
 }
 
 }  // namespace
 
-__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats,
+__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats, bool img,
                                                                   const void* params, dim3 grid, uint32_t lds,
                                                                   hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  if (deep) return B == kDeepLevels ? go_b<kDeepLevels, true>(lvl, stats, params, grid, lds, s, e0, e1) : hipErrorInvalidValue;
+  if (deep) return B == kDeepLevels ? go_b<kDeepLevels, true>(lvl, stats, img, params, grid, lds, s, e0, e1) : hipErrorInvalidValue;
   switch (B) {
-    case 0: return go_b<0, false>(lvl, stats, params, grid, lds, s, e0, e1);
-    case 1: return go_b<1, false>(lvl, stats, params, grid, lds, s, e0, e1);
-    case 2: return go_b<2, false>(lvl, stats, params, grid, lds, s, e0, e1);
-    case 3: return go_b<3, false>(lvl, stats, params, grid, lds, s, e0, e1);
-    case 4: return go_b<4, false>(lvl, stats, params, grid, lds, s, e0, e1);
-    case 5: return go_b<5, false>(lvl, stats, params, grid, lds, s, e0, e1);
-    case 6: return go_b<6, false>(lvl, stats, params, grid, lds, s, e0, e1);
+    case 0: return go_b<0, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
+    case 1: return go_b<1, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
+    case 2: return go_b<2, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
+    case 3: return go_b<3, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
+    case 4: return go_b<4, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
+    case 5: return go_b<5, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
+    case 6: return go_b<6, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
     default: return hipErrorInvalidValue;
   }
 }

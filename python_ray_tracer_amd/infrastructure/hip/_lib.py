@@ -43,6 +43,7 @@ ST_BAD_SCENE = 4
 ST_UNRENDERED = 8  # RTX_F_NO_GENERAL render deferred rays: those pixels are unwritten
 
 F_NO_GENERAL = 1  # rtx_render_camera_ex flags
+F_IMAGES = 2  # RTX_F_IMAGES: the texturing build of the fast kernel (scenes with image textures)
 F_RESERVE_SHIFT = 4  # RTX_F_RESERVE(n) = (n & 0xFFF) << 4
 
 # header words

@@ -213,7 +213,8 @@ class HipRenderer(Renderer):
     """MI355X renderer behind the reference ``Renderer`` plugin surface (application.py:7-32)."""
 
     def __init__(self, max_bounces: int | None = None, *, color_dtype: torch.dtype = torch.float64,
-                 device=None, collect_stats: bool = False, learn_tile_order: bool = True) -> None:
+                 device=None, collect_stats: bool = False, learn_tile_order: bool = True,
+                 fast_textures: bool = True) -> None:
         self._lib = L.load()
         if not torch.cuda.is_available():
             raise RuntimeError("HipRenderer needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")
@@ -230,6 +231,9 @@ class HipRenderer(Renderer):
         # camera launches: the dispatch order learnt per (scene, tile, cap), see _sched_plan
         self.learn_tile_order = bool(learn_tile_order)
         self._sched: dict = {}
+        # scenes with image textures: the fast kernel's texturing build (RTX_F_IMAGES) shades them;
+        # False defers those pixels to the general kernel (same colours)
+        self.fast_textures = bool(fast_textures)
         self._ws = None
         self.stats_buffer = torch.zeros(L.S_WORDS, dtype=torch.int64, device=self.device) if collect_stats else None
 
@@ -390,11 +394,14 @@ class HipRenderer(Renderer):
         rows = n_local_rows(H, row_block, n_parts, part, part_run)
         ws = self.workspace(int(scene.camera.width) * rows)
         flags, probe, order, cost = 0, None, None, None
+        if key is not None and self.fast_textures and any(sp[2][0] == L.TEX_IMAGE for sp in key[0][0]):
+            flags = L.F_IMAGES  # image-textured spheres shaded by the fast kernel, not deferred
         capped = self.max_bounces is not None and self.max_bounces <= L.FAST_MAX_BOUNCES
         if key is not None and self.stats_buffer is None:
             key = (key, row_block, n_parts, part, part_run, self.max_bounces)
             if capped:
-                flags, probe = self._general_plan(key)
+                gflags, probe = self._general_plan(key)
+                flags |= gflags
             if self.learn_tile_order:
                 order, cost = self._sched_plan(key, int(scene.camera.width), rows, n_spheres)
         return blob, n_spheres, rows, ws, flags, probe, key, order, cost

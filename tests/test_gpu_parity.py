@@ -125,7 +125,7 @@ def test_camera_ex_flags_are_checked(hip):
     out = torch.empty((3, 128), dtype=torch.float64, device="cuda")
     ws = r.workspace(128)
     rc = r._lib.rtx_render_camera_ex(blob.data_ptr(), S, 16, 8, 1, 1, 0, 8, 2, out.data_ptr(), L.OUT_F64_SOA,
-                                     ws.data_ptr(), ws.numel(), None, L.stream_handle(), 2, None)
+                                     ws.data_ptr(), ws.numel(), None, L.stream_handle(), 4, None)
     assert rc != 0 and b"flags" in r._lib.rtx_last_error()
     # the deferred count lands in a device word: 0 for a tie-free scene
     cnt = torch.full((1,), -1, dtype=torch.int32, device="cuda")
@@ -580,6 +580,40 @@ def test_image_textured_spheres(hip, B):
     r2 = hip.HipRenderer(max_bounces=B)
     got2 = r2.render(scene2).data.cpu().numpy()
     assert np.abs(got2 - got).max() <= ATOL
+
+
+@pytest.mark.parametrize("B", [1, 3, 5])
+def test_fast_kernel_texturing_build(hip, B):
+    """RTX_F_IMAGES: the capped fast kernel's texturing build shades image-textured hits itself
+    (HipRenderer(fast_textures=True), the default) — whole frames and row tiles bit-identical to
+    the renders that defer those pixels to the general kernel, and fewer pixels deferred (the
+    textured hits stay in the fast kernel)."""
+    from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+    for W, H, S in ((160, 90, None), (96, 64, 40)):  # 40 spheres: the persistent culled kernel
+        spec = _textured_spec(W, H)
+        if S:
+            extra = scenes.random_spec(S, 3, W, H)
+            spec = dict(spec, spheres=spec["spheres"] + extra["spheres"][:S - len(spec["spheres"])])
+        scene = scenes.build_scene(spec)
+        fast = hip.HipRenderer(max_bounces=B, color_dtype=torch.float32)
+        slow = hip.HipRenderer(max_bounces=B, color_dtype=torch.float32, fast_textures=False)
+        assert torch.equal(fast.render(scene).data, slow.render(scene).data), (B, S)
+        for P, part in ((3, 1), (4, 3)):
+            assert torch.equal(fast.render_tile(scene, 8, P, part, out="u8"),
+                               slow.render_tile(scene, 8, P, part, out="u8")), (B, S, P)
+        blob, n = fast.scene_blob(scene)
+        ws = fast.workspace(W * H)
+        out = torch.empty((3, W * H), dtype=torch.float32, device=fast.device)
+        word = torch.full((1,), 7, dtype=torch.int32, device=fast.device)
+        deferred = []
+        for flags in (L.F_IMAGES, 0):
+            L.check(fast._lib.rtx_render_camera_ex(blob.data_ptr(), n, W, H, 1, 1, 0, H, B, out.data_ptr(),
+                                                   L.OUT_F32_SOA, ws.data_ptr(), ws.numel(), None,
+                                                   fast._stream(), flags, word.data_ptr()), "rtx_render_camera_ex")
+            torch.cuda.synchronize()
+            deferred.append(int(word.item()))
+        assert deferred[0] < deferred[1], (B, S, deferred)  # the textured hits no longer deferred
 
 
 @pytest.mark.parametrize("B", [3, None])

@@ -97,7 +97,7 @@ def test_sched_and_tiles_entry_points_validate_on_host():
     lib = L.load()
     text = (REPO / "include" / "rtx_hip.h").read_text()
     for name, val in (("RTX_TILES_LOOPBACK", L.TILES_LOOPBACK), ("RTX_TILES_ROWS", L.TILES_ROWS),
-                      ("RTX_F_RESERVE_SHIFT", L.F_RESERVE_SHIFT), ("RTX_TILES_MAX_SLOTS", L.TILES_MAX_SLOTS)):
+                      ("RTX_F_RESERVE_SHIFT", L.F_RESERVE_SHIFT), ("RTX_F_IMAGES", L.F_IMAGES), ("RTX_TILES_MAX_SLOTS", L.TILES_MAX_SLOTS)):
         assert int(re.search(rf"#define\s+{name}\s+(\d+)", text).group(1)) == val, name
     n = ctypes.c_int64()
     # a persistent launch (>= 32 spheres) hands out 8x8 wave tiles
