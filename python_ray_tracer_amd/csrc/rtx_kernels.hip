@@ -946,9 +946,9 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
 // Colour of one shaded hit given the reflected colour R (shader.py:86-110):
 //   ((((0.004 + diffuse) + dome) + (spec + R*0.5)*g*lit) + irid)
 // `weighted` = lit && g != 0; otherwise the specular/reflection term is x*0 == 0 (R is finite).
-// IMG: image textures are handled (the general kernel); k_render_fast defers every pixel that
-// meets an image-textured sphere, so its instantiations compile no texture lookup (A/B: carrying
-// the lookup cost C2 +3.4%, C2main +7%).
+// IMG: image textures are handled (the general kernel, and k_render_fast's texturing build for
+// RTX_F_IMAGES launches); the other k_render_fast builds defer every pixel that meets an
+// image-textured sphere and compile no texture lookup (A/B: carrying it cost C2 +3.4%, C2main +7%).
 template <bool IMG = false, typename M>
 __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double dli, double di, int tk, bool lit,
                                           bool weighted, double spec, double va, double Rr, double Rg, double Rb,
@@ -1224,7 +1224,7 @@ __device__ __forceinline__ void shade(const cdouble* sc, const G* geo, const T* 
   const double tex = mh[RTX_M_TEX];
   s.tk = tex == RTX_TEX_CHECKER ? (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0))  // :30
          : tex != RTX_TEX_IMAGE ? 0
-         : IMG ? image_texel(mh, gh, px, py, pz) : -1;  // -1: k_render_fast defers the ray
+         : IMG ? image_texel(mh, gh, px, py, pz) : -1;  // -1: an untextured k_render_fast build defers the ray
   s.lit = lit;
   s.qx = qx; s.qy = qy; s.qz = qz;
   s.nx = nx; s.ny = ny; s.nz = nz;
