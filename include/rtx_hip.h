@@ -192,7 +192,9 @@ enum {
   RTX_S_HITS = 72,    /* [72 .. 72+64): shaded hits (= shadow rays) per level */
   RTX_S_WTRACE = 136, /* [136 .. 136+64): waves that traced a level (any lane live), fast kernel */
   RTX_S_WSHADE = 200, /* [200 .. 200+64): waves that shaded a level (any lane hit), fast kernel  */
-  RTX_S_WORDS = 264
+  RTX_S_BOXES = 264,  /* of RTX_S_NODES, the culling tree's box tests (the rest are frustum-plane, shadow-grid
+                         and beam work priced as node tests)                                       */
+  RTX_S_WORDS = 265
 };
 
 /* workspace: status words then deferred-ray list then per-worker frame stacks.

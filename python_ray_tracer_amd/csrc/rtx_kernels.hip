@@ -528,13 +528,17 @@ template <bool ON>
 struct Work {
   __device__ __forceinline__ void test(int) {}
   __device__ __forceinline__ void node() {}
+  __device__ __forceinline__ void box() {}
 };
 template <>
 struct Work<true> {
   uint32_t tests = 0, nodes = 0;
   uint32_t tests1 = 0, nodes1 = 0;  // of the nearest-hit searches of reflected rays (levels >= 1)
+  uint32_t boxes = 0;  // of the node tests, the culling tree's box tests (the rest: frustum planes,
+                       // shadow-grid lookups, beam passes, priced as node tests)
   __device__ __forceinline__ void test(int k) { tests += (uint32_t)k; }
   __device__ __forceinline__ void node() { ++nodes; }
+  __device__ __forceinline__ void box() { ++boxes; }
 };
 
 // Shadow any-hit: does test j (root t, validity v) come strictly before the shape's own distance
@@ -631,6 +635,7 @@ __device__ __forceinline__ void nearest_bvh(const cdouble* sc, double ox, double
   while (i < nn) {
     const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
     wk.node();
+    wk.box();
     if (__ballot(node_may_hit(nd, ox, oy, oz, rs, tmin)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
       if (cnt > 0)
@@ -711,6 +716,7 @@ __device__ __forceinline__ bool lit_bvh(const cdouble* sc, double qx, double qy,
   while (i < nn) {
     const cdouble* nd = nodes + __builtin_amdgcn_readfirstlane(i) * RTX_NODE_WORDS;
     wk.node();
+    wk.box();
     if (__ballot(lit && node_may_hit(nd, qx, qy, qz, rs, tself)) != 0) {
       const int cnt = (int)nd[RTX_N_COUNT];
       if (cnt > 0) {
@@ -1841,6 +1847,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_add(st, RTX_S_NODES, wk.nodes);
       stat_add(st, RTX_S_TESTS1, wk.tests1);
       stat_add(st, RTX_S_NODES1, wk.nodes1);
+      stat_add(st, RTX_S_BOXES, wk.boxes);
     }
   }
   if (deferred) {

@@ -42,7 +42,9 @@ def test_render_tile_trace_match_hiprenderer(env):
         r64 = H.HipRenderer(max_bounces=B)
         assert torch.equal(torch.ops.rt.render_tile(blob, S, 200, 117, 8, 3, 2, bl, 1, ws), r64.render_tile(scene, 8, 3, 2))
         # per-level counters through the optional stats tensor
-        st = torch.zeros(264, dtype=torch.int64, device="cuda")
+        from python_ray_tracer_amd.infrastructure.hip import _lib as L
+
+        st = torch.zeros(L.S_WORDS, dtype=torch.int64, device="cuda")
         torch.ops.rt.render_tile(blob, S, 200, 117, 1, 1, 0, bl, 0, ws, st)
         ost = O.TraceStats()
         O.render(O.scene_from_spec(spec), B, stats=ost)

@@ -62,6 +62,7 @@ def test_abi_layout_matches_header():
     assert const("RTX_GEOM_WORDS") == L.GEOM_WORDS
     assert const("RTX_MAT_WORDS") == L.MAT_WORDS
     assert const("RTX_S_WORDS") == L.S_WORDS
+    assert const("RTX_S_BOXES") == L.S_BOXES
     assert const("RTX_H_CAMOO") == L.H_CAMOO
     assert const("RTX_M_TFIOR") == L.M_TFIOR
     assert const("RTX_G_C0") == L.G_C0
@@ -391,7 +392,7 @@ def test_torch_ops_schema_and_fake_kernels():
     meta = {"device": "meta"}
     blob = torch.empty(64 + 3 * 32, dtype=torch.float64, **meta)
     ws = torch.empty(1 << 20, dtype=torch.uint8, **meta)
-    st = torch.empty(264, dtype=torch.int64, **meta)
+    st = torch.empty(L.S_WORDS, dtype=torch.int64, **meta)
     assert torch.ops.rt.render_tile(blob, 3, 20, 17, 1, 1, 0, 3, 0, ws, st).shape == (3, 340)
     out = torch.ops.rt.render_tile(blob, 3, 20, 17, 4, 3, 1, 3, 2, ws)  # rows 4-7 and 16: 5 rows
     assert out.shape == (5, 20, 3) and out.dtype == torch.uint8
