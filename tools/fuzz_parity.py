@@ -6,7 +6,8 @@ Each case draws a scene like tests/test_gpu_parity.py's fuzz generator but wider
 radius 1e-3 .. 150 (some centred on or touching the camera, some far beyond 2^60 so the scene is
 untamed), random lights, domes, cameras and frame sizes, and a cap in 0..12 or unbounded. The
 HIP render must match the oracle within 1e-12 with identical uint8 pixels and equal per-level
-ray/hit counters. Prints one JSON summary line (and writes it to --out)."""
+ray/hit counters, and the timed kernels (no counters: learnt dispatch order, general-kernel probe,
+weighted row shares re-assembled) must give the same frame bit for bit. Prints one JSON summary line (and writes it to --out)."""
 
 import argparse
 import json
@@ -19,7 +20,7 @@ import numpy as np
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 from oracle import numpy_oracle as O  # noqa: E402
-from python_ray_tracer_amd import scenes  # noqa: E402
+from python_ray_tracer_amd import scenes, tiling  # noqa: E402
 
 
 def make_spec(seed, scale=1):
@@ -69,6 +70,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--seeds", default=None, help="comma list: only these seeds")
     ap.add_argument("--scale", type=int, default=1, help="frame size multiplier")
+    ap.add_argument("--no-timed", dest="timed", action="store_false",
+                    help="skip the timed-kernel checks (learnt order, probe, weighted row shares)")
     a = ap.parse_args()
     import torch
 
@@ -108,11 +111,30 @@ def main():
         u8 = np.array_equal(O.to_uint8(got, W, Hh), O.to_uint8(want, W, Hh))
         # the kernel records the first RTX_S_LEVELS (64) levels; longer unbounded chains stop there
         cnt = s["rays"] == st.rays[:64] and s["hits"] == st.hits[:64]
-        ok = err <= 1e-12 and u8 and cnt
+        # the timed kernels (no counters: the learnt order, the general-kernel probe, weighted row
+        # shares) must give the counting render's frame bit for bit
+        timed = True
+        if a.timed:
+            r2 = H.HipRenderer(max_bounces=B)
+            ref = torch.from_numpy(got).to(r2.device)
+            for _ in range(3):  # first launch learns the order and probes; later ones use both
+                timed = timed and torch.equal(r2.render_tile(scene), ref)
+            for world, root_run, run in ((4, 1, 2), (3, 2, 3)):
+                n_parts, shares = tiling.runs(world, root_run, run)
+                for rb in (1, 4):
+                    plen = tiling.part_len(Hh, W, rb, world, 8, None, root_run, run)
+                    buf = torch.zeros((world, plen), dtype=torch.float64, device=r2.device)
+                    for q, (first, k_run) in enumerate(shares):
+                        shp = tiling.tile_shape(Hh, W, rb, n_parts, first, None, k_run)
+                        r2.render_tile(scene, rb, n_parts, first, into=buf[q, :int(np.prod(shp))].view(shp),
+                                       part_run=k_run)
+                    timed = timed and torch.equal(r2.assemble_rows(buf, W, Hh, rb, None, root_run, run), ref)
+        ok = err <= 1e-12 and u8 and cnt and timed
         worst = max(worst, err)
         pixels += W * Hh
         if not ok:
             fails.append({"seed": seed, "B": B, "err": err, "uint8_equal": bool(u8), "counters_equal": bool(cnt),
+                          "timed_kernels_equal": bool(timed),
                           "rays": [s["rays"], st.rays] if not cnt else None,
                           "hits": [s["hits"], st.hits] if not cnt else None})
         if k % 50 == 49:
