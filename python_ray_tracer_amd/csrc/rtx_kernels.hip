@@ -2579,12 +2579,13 @@ static_assert(RTX_FAST_MAX_BOUNCES == 6, "launch_fast switch covers 0..6");
 // no_general: the caller knows this exact (capped) render defers no ray (rtx_render_camera_ex)
 int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {
   if (p.nsph <= 0 || p.nsph > RTX_MAX_SPHERES) return fail(RTX_E_ARG, "n_spheres out of range%s (%lld)", "", p.nsph);
-  if (!p.scene || !p.out || !workspace) return fail(RTX_E_ARG, "null pointer argument%s", "");
+  if (!p.scene || !workspace) return fail(RTX_E_ARG, "null pointer argument%s", "");
   if (p.out_kind < 0 || p.out_kind > 2) return fail(RTX_E_ARG, "bad out_kind%s %lld", "", p.out_kind);
   if (p.max_bounces < RTX_UNBOUNDED) return fail(RTX_E_ARG, "bad max_bounces%s %lld", "", p.max_bounces);
   if (p.n_frames <= 0) p.n_frames = 1;
   if (p.n_frames > 65535) return fail(RTX_E_ARG, "at most 65535 frames per launch%s (%lld)", "", p.n_frames);
-  if (p.n <= 0) return RTX_OK;
+  if (p.n <= 0) return RTX_OK;  // (an empty tile, e.g. a rank's share of a small frame: out may be null)
+  if (!p.out) return fail(RTX_E_ARG, "null pointer argument%s", "");
   if (p.n >= (int64_t(1) << kFrameShift)) return fail(RTX_E_ARG, "too many pixels per frame%s (%lld)", "", p.n);
   const int64_t n_all = p.n * p.n_frames;  // pixels of the whole launch
   const size_t need = ws_bytes(n_all, p.max_bounces);

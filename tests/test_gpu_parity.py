@@ -209,6 +209,18 @@ def test_row_tile_shares_reassemble(hip):
             case = (world, root_run, run, rb, out)
             assert torch.equal(r.assemble_rows(buf, 200, 117, rb, out, root_run, run), ref), case
             assert torch.equal(tiling.assemble(buf.cpu(), 117, 200, rb, out, root_run, run), ref.cpu()), case
+    # a frame smaller than one cycle: the root's share holds every row, the peers' are empty (their
+    # launches render nothing; an empty output needs no buffer)
+    small = scenes.build_scene(scenes.readme_spec(40, 10))
+    want = r.render(small).data
+    n_parts, shares = tiling.runs(3, 2, 3)
+    buf = torch.zeros((3, tiling.part_len(10, 40, 8, 3, 4, None, 2, 3)), dtype=torch.float32, device=want.device)
+    for k, (first, k_run) in enumerate(shares):
+        shp = tiling.tile_shape(10, 40, 8, n_parts, first, None, k_run)
+        assert (shp[1] == 0) == (k > 0), shp
+        r.render_tile(small, 8, n_parts, first, into=buf[k, :int(np.prod(shp))].view(shp), part_run=k_run)
+        assert r.render_tile(small, 8, n_parts, first, part_run=k_run).shape == shp
+    assert torch.equal(r.assemble_rows(buf, 40, 10, 8, None, 2, 3), want)
 
 
 def test_render_batch_matches_single_frames(hip):
