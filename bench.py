@@ -367,10 +367,11 @@ def main():
         dist.destroy_process_group()
 
 
-def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=None, rows=None):
+def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=None, rows=None, timed=False):
     """(step, drain) of the strong-scaling tiles mode: TileGather with two slots; step k submits
     frame k and finishes frame k-1 (its gather overlapped frame k's render); drain finishes the last
-    one. Without a process group: the whole frame rendered into a pre-allocated buffer."""
+    one. Without a process group: the whole frame rendered into a pre-allocated buffer. ``timed``:
+    the plan records its gathers (RTX_TILES_TIMED); ``step.timing()`` reads the last frame's."""
     import torch
     import torch.distributed as dist
 
@@ -385,16 +386,19 @@ def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=
     from python_ray_tracer_amd.distributed import TileGather
 
     tg = TileGather(r, int(scene.camera.width), int(scene.camera.height), row_block=row_block, out=out, slots=2,
-                    persistent_frames=True, loopback=loopback, comm_reserve=comm_reserve, rows=rows)
-    state = {"k": 0, "open": None}
+                    persistent_frames=True, loopback=loopback, comm_reserve=comm_reserve, rows=rows, timed=timed)
+    state = {"k": 0, "open": None, "last": None}
 
     def step():
         slot = state["k"] % 2
         tg.submit(scene, slot)
         if state["open"] is not None:
             tg.finish(state["open"])
-        state["open"] = slot
+        state["open"] = state["last"] = slot
         state["k"] += 1
+
+    step.tg = tg
+    step.timing = lambda: tg.timing(state["last"])
 
     def drain():
         if state["open"] is not None:
@@ -469,13 +473,21 @@ def secondary_tiles(args, r, scene, world, dev, coll_dev):
         c4spec, c4B = scenes.CONFIGS["C4"]()
         r4 = HipRenderer(max_bounces=c4B, color_dtype=torch.float32, device=dev,
                          learn_tile_order=not args.no_tile_order)
-        step, drain = tiles_stepper(r4, scenes.build_scene(c4spec), world, args.row_block, "u8")
+        # N = 1: a loopback plan (the tile still goes through RCCL, sent to and received from the
+        # rank itself, then assembled), so that the one-GPU point runs the gather path of N > 1
+        loop = world == 1 and dist.get_backend() == "nccl"
+        step, drain = tiles_stepper(r4, scenes.build_scene(c4spec), world, args.row_block, "u8", loopback=loop,
+                                    timed=dist.get_backend() == "nccl")
         k4 = 10
         t = timed(step, drain, k4, 2)
         out["c4_tiles"] = {"value": round(7680 * 4320 * k4 / t / 1e6, 3), "unit": "Mpixels/s",
                            "ms_per_step": round(t / k4 * 1e3, 5), "steps": k4, "scaling": "strong",
                            "config": "C4: 64 random spheres + ground 7680x4320 seed 0, 5 bounces, row-tiled over "
-                                     f"{world} rank(s), gather of the uint8 frame to rank 0"}
+                                     f"{world} rank(s), gather of the uint8 frame to rank 0"
+                                     + (" (one-rank loopback plan: the tile sent to and received from the rank "
+                                        "itself over RCCL, then assembled)" if loop else "")}
+        if getattr(getattr(step, "tg", None), "timed", False):
+            out["c4_tiles"]["gather"] = gather_timing(step.timing(), world, loop)
         if world > 1:
             # the strong-scaling speed-up in the same run: rank 0 alone renders the whole C4 frame
             # as the one-rank tiles path does (straight into the uint8 frame), the others wait
@@ -494,11 +506,42 @@ def secondary_tiles(args, r, scene, world, dev, coll_dev):
                 out["c4_tiles"]["speedup_vs_1gpu"] = round(t1 / (t / k4), 4)
             dist.barrier()
     except Exception as e:  # noqa: BLE001
+        if world > 1:
+            # N > 1: the row-tiled frame is the north star's multi-GPU mechanism; a broken plan must
+            # fail the run (non-zero exit), not hide behind a green headline
+            raise
         out["tiles_error"] = repr(e)[:300]
     finally:
         if own_group:
             dist.destroy_process_group()
     return out
+
+
+def gather_timing(mine: dict, world: int, loop: bool) -> dict:
+    """The C4 tiles leg's measured gather (rtx_tiles_timing on every rank, last timed frame):
+    bytes per peer, the root's span (its tile rendered -> every part received) and its assembly,
+    each peer's send span (its tile rendered -> delivered; the root's receive is posted when the
+    root's smaller share has rendered), and the achieved rate per link = part bytes / send span."""
+    import torch.distributed as dist
+
+    allt = [mine]
+    if world > 1:
+        allt = [None] * world
+        dist.all_gather_object(allt, mine)
+    root = allt[0]
+    g = {"part_bytes": root["part_bytes"], "root_gather_ms": round(root["gather_ms"], 4),
+         "root_assemble_ms": round(root["assemble_ms"], 4), "root_received_bytes": root["bytes"]}
+    if loop:
+        g["link"] = "loopback: RCCL send/recv to the same GPU (HBM to HBM), not an xGMI link"
+        g["loopback_GBps"] = round(root["part_bytes"] / max(root["gather_ms"], 1e-6) / 1e6, 2)
+    else:
+        peers = [a["gather_ms"] for a in allt[1:]]
+        g["link"] = "xGMI point-to-point, one peer per link into the root"
+        g["peer_send_ms"] = [round(x, 4) for x in peers]
+        g["link_GBps_per_peer"] = [round(root["part_bytes"] / max(x, 1e-6) / 1e6, 2) for x in peers]
+        g["link_GBps_min"] = min(g["link_GBps_per_peer"]) if peers else None
+        g["root_in_GBps"] = round(root["bytes"] / max(root["gather_ms"], 1e-6) / 1e6, 2)
+    return g
 
 
 def emulate_parts(args, r, scene, spec, B, part_counts):

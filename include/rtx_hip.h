@@ -385,6 +385,10 @@ int rtx_comm_destroy(void* comm);
  * copy), so the root never runs the assembly pass (a read and a write of the whole frame in HBM,
  * beside its next render). recv[s] then holds the root's own tile only (part_bytes). */
 #define RTX_TILES_ROWS 2u
+/* RTX_TILES_TIMED: timing events on the plan's stream around each slot's RCCL group and the root's
+ * assembly (plans that gather), read back by rtx_tiles_timing: the measured gather per frame and
+ * rank (bench.py's secondary.c4_tiles.gather: bytes per peer and the achieved rate per link). */
+#define RTX_TILES_TIMED 4u
 /* Shares: rank 0 renders the run of parts [0, root_run) and rank i >= 1 the run [root_run + (i - 1)
  * run, root_run + i run) of the root_run + (world - 1) run interleave (rtx_render_camera_sched
  * part_run). root_run = run = 1 is the even split; a root_run below run leaves the root, which also
@@ -413,6 +417,12 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
 int rtx_tiles_finish(void* plan, int slot, void* stream);
 /* Waits for the plan's stream, then frees its stream and events (not the caller's buffers). */
 int rtx_tiles_destroy(void* plan);
+/* RTX_TILES_TIMED plans: waits for slot `slot`'s latest frame on the plan's stream, then gives
+ * gather_ms, from the moment the plan's stream could start the gather (this rank's tile rendered)
+ * to the completion of its RCCL group (a peer: its send delivered; the root: every peer's tile
+ * received), and assemble_ms, the root's assembly after it (0 on peers). Synchronising: call it
+ * outside a timed region. No replacement in the reference (one process, application.py:43-52). */
+int rtx_tiles_timing(void* plan, int slot, float* gather_ms, float* assemble_ms);
 
 /* Test hook: out[0:n] = the library's fast-path sqrt(a), out[n:2n] = the compiler's full sqrt(a),
  * out[2n:3n] = fast-path a/b, out[3n:4n] = full a/b, out[4n:5n] = the renormalisation factor of an

@@ -160,6 +160,29 @@ def build_ops(force: bool = False, verbose: bool = False) -> Path:
     return OPS_LIB
 
 
+STUB_SRC = REPO / "tests" / "stub_rccl.cpp"  # test-only RCCL stand-in (world > 1 tiles plans on one GPU)
+STUB_LIB = REPO / "tests" / "libstub_rccl.so"
+
+
+def build_test_stub(force: bool = False, verbose: bool = False) -> Path:
+    """tests/libstub_rccl.so: the test-only RCCL stand-in the world > 1 tiles tests bind through
+    rtx_rccl_load(path) (host code; -Bsymbolic so its own calls never resolve to torch's librccl)."""
+    if not force and STUB_LIB.exists() and STUB_SRC.stat().st_mtime <= STUB_LIB.stat().st_mtime:
+        return STUB_LIB
+    tmp = STUB_LIB.with_suffix(f".so.tmp{os.getpid()}")
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wl,-Bsymbolic",
+           "-o", str(tmp), str(STUB_SRC)]
+    if verbose:
+        print(" ".join(cmd))
+    try:
+        subprocess.run(cmd, check=True, cwd=str(REPO))
+        os.replace(tmp, STUB_LIB)
+    finally:
+        tmp.unlink(missing_ok=True)
+    return STUB_LIB
+
+
 if __name__ == "__main__":
     print(build_library(force=True, verbose=True))
     print(build_ops(force=True, verbose=True))
+    print(build_test_stub(force=True, verbose=True))

@@ -2,13 +2,15 @@
 // TORCH_LIBRARY(rt, m) over the C ABI of librtx_hip.so (include/rtx_hip.h).
 //
 //   rt::render_tile   <- NumpyRenderer.get_ray_directions + raytrace_scene, fused, for one interleaved
-//                        row tile of the scene camera's frame (base.py:91-141, shader.py:63-161)
+//                        row tile of the scene camera's frame, or a run of part_run parts (a rank's
+//                        weighted share: rtx_render_camera_sched) (base.py:91-141, shader.py:63-161)
 //   rt::render_frames <- F x render_image_pipeline's render step in one launch (application.py:43-52)
 //   rt::trace         <- NumpyRenderer.raytrace_scene(O, D, scene) on arbitrary rays (base.py:91-121)
 //   rt::shade_hits    <- NumpyShader.create(shape, scene, O, D, t, renderer) (shader.py:63-112)
 //   rt::intersect     <- NumpySphere.intersect (shape.py:28-51)
 //   rt::quantize_u8   <- save_image's (255*clip(c,0,1)).astype(uint8) (base.py:143-151)
-//   rt::assemble_rows <- the multi-GPU frame's row un-permute (application.render_frame_distributed)
+//   rt::assemble_rows <- the multi-GPU frame's row un-permute (application.render_frame_distributed),
+//                        equal shares or weighted ones (root_run / run: rtx_assemble_runs)
 //   rt::status        <- reads and clears the workspace's sticky RTX_ST_* flags
 //   rt::workspace_bytes
 //
@@ -86,8 +88,12 @@ struct CheckedBlob {
   int64_t numel = -1, version = -1, n_spheres = -1;
   bool matches(const at::Tensor& t, int64_t ns) const {
     return !impl.expired() && impl._unsafe_get_target() == t.unsafeGetTensorImpl() && data == t.data_ptr() &&
-           numel == t.numel() && version == t._version() && n_spheres == ns;
+           numel == t.numel() && version == version_of(t) && n_spheres == ns;
   }
+  // inference tensors keep no version counter (_version() throws): they are keyed on the object, its
+  // storage and size alone (a blob rewritten in place under inference_mode is caught by the kernel's
+  // own header test, RTX_ST_BAD_SCENE, which renders nothing)
+  static int64_t version_of(const at::Tensor& t) { return t.is_inference() ? -2 : (int64_t)t._version(); }
 };
 constexpr int kCheckedBlobs = 32;
 std::mutex g_checked_mu;
@@ -117,7 +123,7 @@ void check_headers(const at::Tensor& blobs, int64_t n_spheres) {
   c.impl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>(blobs.getIntrusivePtr());
   c.data = blobs.data_ptr();
   c.numel = blobs.numel();
-  c.version = blobs._version();
+  c.version = CheckedBlob::version_of(blobs);
   c.n_spheres = n_spheres;
 }
 
@@ -136,9 +142,17 @@ void check_status_after(at::Tensor& ws, int64_t max_bounces) {
   TORCH_CHECK(false, "render status flags ", st, " (RTX_ST_LIST_OVERFLOW: deferred list full)");
 }
 
-int64_t tile_rows(int64_t height, int64_t row_block, int64_t n_parts, int64_t part) {
-  const int64_t cycle = row_block * n_parts, q = height / cycle, rem = height % cycle - part * row_block;
-  return q * row_block + (rem < 0 ? 0 : rem > row_block ? row_block : rem);
+// local rows of the run of `run` parts from `part` (tiling.n_local_rows)
+int64_t tile_rows(int64_t height, int64_t row_block, int64_t n_parts, int64_t part, int64_t run = 1) {
+  const int64_t cycle = row_block * n_parts, own = row_block * run, q = height / cycle,
+                rem = height % cycle - part * row_block;
+  return q * own + (rem < 0 ? 0 : rem > own ? own : rem);
+}
+
+void check_tile(int64_t width, int64_t height, int64_t row_block, int64_t n_parts, int64_t part, int64_t part_run) {
+  TORCH_CHECK(width > 0 && height > 0 && row_block > 0 && n_parts > 0 && part >= 0 && part_run >= 1 &&
+                  part + part_run <= n_parts,
+              "bad frame/tile geometry (part ", part, ", part_run ", part_run, " of ", n_parts, " parts)");
 }
 
 // frames: 0 = a single output, F > 0 = [F, ...] outputs of F frames
@@ -203,21 +217,22 @@ int64_t check_rays(const at::Tensor& scene, const at::Tensor& origins, const at:
 
 at::Tensor render_tile(const at::Tensor& scene, int64_t n_spheres, int64_t width, int64_t height, int64_t row_block,
                        int64_t n_parts, int64_t part, int64_t max_bounces, int64_t out_kind, at::Tensor& workspace,
-                       const std::optional<at::Tensor>& stats, bool check) {
+                       const std::optional<at::Tensor>& stats, bool check, int64_t part_run) {
   check_scene(scene, n_spheres);
   const at::OptionalDeviceGuard guard(at::device_of(scene));
-  TORCH_CHECK(width > 0 && height > 0 && row_block > 0 && n_parts > 0 && part >= 0 && part < n_parts,
-              "bad frame/tile geometry");
+  check_tile(width, height, row_block, n_parts, part, part_run);
   check_bounces(max_bounces);
-  const int64_t rows = tile_rows(height, row_block, n_parts, part);
+  const int64_t rows = tile_rows(height, row_block, n_parts, part, part_run);
   const int64_t n = width * rows;
   check_workspace(workspace, scene, n, max_bounces);
   if (check) check_headers(scene, n_spheres);
   at::Tensor out = new_output(scene, n, rows, width, out_kind);
-  check_rc(rtx_render_camera(scene.data_ptr<double>(), (int)n_spheres, (int)width, (int)height, (int)row_block,
-                             (int)n_parts, (int)part, (int)rows, (int)max_bounces, out.data_ptr(), (int)out_kind,
-                             workspace.data_ptr(), (size_t)workspace.numel(), stats_ptr(stats, scene), stream_of(scene)),
-           "rtx_render_camera");
+  // a run of parts (a rank's weighted share, distributed.ROOT_SHARES) in one launch; bottom-up order
+  check_rc(rtx_render_camera_sched(scene.data_ptr<double>(), (int)n_spheres, (int)width, (int)height, (int)row_block,
+                                   (int)n_parts, (int)part, (int)part_run, (int)rows, (int)max_bounces, out.data_ptr(),
+                                   (int)out_kind, workspace.data_ptr(), (size_t)workspace.numel(),
+                                   stats_ptr(stats, scene), stream_of(scene), 0u, nullptr, nullptr, nullptr),
+           "rtx_render_camera_sched");
   if (check) check_status_after(workspace, max_bounces);
   return out;
 }
@@ -335,13 +350,19 @@ at::Tensor assemble_out(const at::Tensor& tiles, int64_t width, int64_t height, 
   return at::empty({3, height * width}, tiles.options());
 }
 
-at::Tensor assemble_rows(const at::Tensor& tiles, int64_t width, int64_t height, int64_t row_block, int64_t out_kind) {
+at::Tensor assemble_rows(const at::Tensor& tiles, int64_t width, int64_t height, int64_t row_block, int64_t out_kind,
+                         int64_t root_run, int64_t run) {
   TORCH_CHECK(on_gpu(tiles), "tiles must be a contiguous [P, L] GPU tensor");
+  TORCH_CHECK(root_run >= 1 && run >= 1, "root_run and run must be >= 1");
   const at::OptionalDeviceGuard guard(at::device_of(tiles));
   at::Tensor out = assemble_out(tiles, width, height, out_kind);
-  check_rc(rtx_assemble_rows(tiles.data_ptr(), tiles.stride(0) * (int64_t)tiles.element_size(), (int)tiles.size(0),
-                             (int)width, (int)height, (int)row_block, (int)out_kind, out.data_ptr(), stream_of(tiles)),
-           "rtx_assemble_rows");
+  // rank i's tile at row i (its run of parts: rank 0 parts [0, root_run), rank i >= 1 the run
+  // [root_run + (i - 1) run, + run) of the root_run + (P - 1) run interleave); equal runs of one
+  // part are rtx_assemble_rows
+  check_rc(rtx_assemble_runs(tiles.data_ptr(), tiles.stride(0) * (int64_t)tiles.element_size(), (int)tiles.size(0),
+                             (int)root_run, (int)run, (int)width, (int)height, (int)row_block, (int)out_kind,
+                             out.data_ptr(), stream_of(tiles)),
+           "rtx_assemble_runs");
   return out;
 }
 
@@ -363,11 +384,10 @@ int64_t workspace_bytes(int64_t n_rays, int64_t max_bounces) {
 
 at::Tensor render_tile_meta(const at::Tensor& scene, int64_t n_spheres, int64_t width, int64_t height,
                             int64_t row_block, int64_t n_parts, int64_t part, int64_t, int64_t out_kind, at::Tensor&,
-                            const std::optional<at::Tensor>&, bool) {
+                            const std::optional<at::Tensor>&, bool, int64_t part_run) {
   check_scene_shape(scene, n_spheres);
-  TORCH_CHECK(width > 0 && height > 0 && row_block > 0 && n_parts > 0 && part >= 0 && part < n_parts,
-              "bad frame/tile geometry");
-  const int64_t rows = tile_rows(height, row_block, n_parts, part);
+  check_tile(width, height, row_block, n_parts, part, part_run);
+  const int64_t rows = tile_rows(height, row_block, n_parts, part, part_run);
   return new_output(scene, width * rows, rows, width, out_kind);
 }
 
@@ -400,7 +420,9 @@ at::Tensor quantize_u8_meta(const at::Tensor& color) {
   return at::empty({color.size(1), 3}, color.options().dtype(at::kByte));
 }
 
-at::Tensor assemble_rows_meta(const at::Tensor& tiles, int64_t width, int64_t height, int64_t, int64_t out_kind) {
+at::Tensor assemble_rows_meta(const at::Tensor& tiles, int64_t width, int64_t height, int64_t, int64_t out_kind,
+                              int64_t root_run, int64_t run) {
+  TORCH_CHECK(root_run >= 1 && run >= 1, "root_run and run must be >= 1");
   return assemble_out(tiles, width, height, out_kind);
 }
 
@@ -408,7 +430,8 @@ at::Tensor assemble_rows_meta(const at::Tensor& tiles, int64_t width, int64_t he
 
 TORCH_LIBRARY(rt, m) {
   m.def("render_tile(Tensor scene, int n_spheres, int width, int height, int row_block, int n_parts, int part, "
-        "int max_bounces, int out_kind, Tensor(a!) workspace, Tensor(b!)? stats=None, bool check=True) -> Tensor");
+        "int max_bounces, int out_kind, Tensor(a!) workspace, Tensor(b!)? stats=None, bool check=True, "
+        "int part_run=1) -> Tensor");
   m.def("render_frames(Tensor scenes, int n_spheres, int width, int height, int max_bounces, int out_kind, "
         "Tensor(a!) workspace, Tensor(b!)? stats=None, bool check=True) -> Tensor");
   m.def("trace(Tensor scene, int n_spheres, Tensor origins, Tensor dirs, int max_bounces, int out_kind, "
@@ -417,7 +440,8 @@ TORCH_LIBRARY(rt, m) {
         "int out_kind, Tensor(a!) workspace, Tensor(b!)? stats=None, bool check=True) -> Tensor");
   m.def("intersect(Tensor sphere, Tensor origins, Tensor dirs) -> Tensor");
   m.def("quantize_u8(Tensor color) -> Tensor");
-  m.def("assemble_rows(Tensor tiles, int width, int height, int row_block, int out_kind) -> Tensor");
+  m.def("assemble_rows(Tensor tiles, int width, int height, int row_block, int out_kind, int root_run=1, "
+        "int run=1) -> Tensor");
   m.def("status(Tensor(a!) workspace) -> int");
   m.def("workspace_bytes(int n_rays, int max_bounces) -> int", &workspace_bytes);
 }

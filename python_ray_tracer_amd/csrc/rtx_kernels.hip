@@ -78,6 +78,18 @@ constexpr int kLvWavesSmall = 5;     // ... and of their TREE = false instantiat
 constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
 constexpr int kDeepWaves = 3;        // waves/SIMD of the DEEP instantiation (records + continuation need registers)
 constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
+// Capped kernels (B <= RTX_FAST_MAX_BOUNCES): the bounce chain's colour is accumulated forwards,
+// col = sum_k T_k L_k with T_0 = 1, T_{k+1} = (T_k * 0.5) * g_k and L_k level k's colour with a
+// black reflection, instead of storing every non-terminal level's colour inputs and folding them
+// back from the deepest level (the reference's association, shader.py:106-110: col_k = ((A_k +
+// (spec_k + col_{k+1} * 0.5) * g_k) + I_k)). Same terms, reassociated: the result moves by a few
+// ulp of the colour (<= ~1e-13 absolute at the brightest unclipped values, under the 1e-12 parity
+// bar), and no level's inputs live in LDS slots or registers across the chain: C4's B = 5 kernel
+// kept three levels in a register shift (27 VGPRs, the bulk of its 41 spilled) beside two LDS slots.
+// The DEEP kernels keep the backward fold (their resume records carry the levels' inputs).
+constexpr bool kForwardFold = true;
+constexpr int kFwdWaves = 4;        // waves/SIMD of the forward-fold kernels with a culling tree
+constexpr int kFwdWavesSmall = 5;   // ... and of their TREE = false instantiations
 constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
                                      // 8-level instantiation spills, 3 defers too many pixels)
 constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k_render_fast<cap>
@@ -117,7 +129,7 @@ constexpr int kLdsMaxSpheres = 128;  // scene table staged in LDS up to this siz
 // slots indexed by the level instead of a register shift register (no moves per level, 27 fewer
 // live VGPRs): [B][4][kFastBlock] doubles + [B][kFastBlock] ints after the scene table.
 template <int B, bool LDS, bool DEEP>
-constexpr bool levels_in_lds() { return kLevelsInLds && LDS && !DEEP && B > 0 && B <= kLevelsLdsMaxB; }
+constexpr bool levels_in_lds() { return kLevelsInLds && LDS && !DEEP && !kForwardFold && B > 0 && B <= kLevelsLdsMaxB; }
 // the DEEP variant (3 waves/SIMD: 3 blocks per CU) keeps all its levels in LDS
 template <bool DEEP = false>
 __host__ __device__ constexpr int level_lds_slots(int B) {
@@ -1704,12 +1716,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const int lt = threadIdx.x;
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
+  // kForwardFold (capped kernels): colour accumulated level by level, thr = T_k
+  constexpr bool FWD = kForwardFold && !DEEP;
+  double thr = 1.0;
   bool deferred = false, appended = false;
   int rays_through = 0, hits_through = -1;  // per-level counts already made for this pixel
 
   for (int k = 0;; ++k) {
     if (hit < 0) {  // nothing hit: NumpyRGBColor(0, 0, 0) (base.py:100)
-      cr = cg = cb = 0.0;
+      if constexpr (!FWD) cr = cg = cb = 0.0;  // (forwards: a black reflection adds nothing)
       break;
     }
     if (tie) {  // several shapes shaded and summed: the general kernel takes this ray
@@ -1771,7 +1786,19 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       }
       break;
     }
-    if (!weighted || k >= B || at_cap) {
+    if (FWD) {
+      // this level's colour with a black reflection, weighted by the chain's throughput (at level 0
+      // cr = 0 + 1 * L_0 = L_0 exactly: a chain of one level is bit-identical to the backward fold)
+      const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
+      double lr_, lg_, lb_;
+      hit_color<IMG>(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
+                     s.va, 0.0, 0.0, 0.0, lr_, lg_, lb_);
+      cr = cr + thr * lr_;
+      cg = cg + thr * lg_;
+      cb = cb + thr * lb_;
+      if (!weighted || k >= B) break;
+      thr = (thr * 0.5) * s.g;  // the reflection's weight, (R * 0.5) * g (shader.py:106)
+    } else if (!weighted || k >= B || at_cap) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
       const double* tab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
       hit_color<IMG>(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
@@ -1779,7 +1806,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       break;
     }
     // push this level's colour inputs; the reflected ray becomes the next level
-    if constexpr (LV) {
+    if constexpr (FWD) {
+      // (nothing to keep: the level's colour is already in cr, cg, cb)
+    } else if constexpr (LV) {
       if (NL == B || k < NL) {  // k: wave-uniform, == depth of every active lane
         double* const l = lvd + (depth * 4) * FB + lt;
         l[0] = s.dli; l[FB] = s.di; l[2 * FB] = s.spec; l[3 * FB] = s.va;
@@ -1802,7 +1831,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       sDli[0] = s.dli; sDi[0] = s.di; sSpec[0] = s.spec; sVa[0] = s.va;
       sKey[0] = level_key(hit, s.tk);
     }
-    ++depth;
+    if constexpr (!FWD) ++depth;
     reflect_dir(dx, dy, dz, s.nx, s.ny, s.nz);
     ox = s.qx;
     oy = s.qy;
@@ -1906,8 +1935,10 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2,
           bool IMG = false>
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
-                             (DEEP ? kDeepWaves : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
-                                                      : kFastWavesPerSimd)) void k_render_fast(Params p0) {
+                             (DEEP  ? kDeepWaves
+                              : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
+                              : kForwardFold ? (TP ? kFwdWaves : kFwdWavesSmall)
+                                             : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   constexpr bool TREE = TP >= 1;
   // reflected-ray beams (wave_beam): scenes of kPersistMinSpheres and more, capped renders (A/B: C4
   // -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%)
@@ -1967,13 +1998,18 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
         (const uint32_t __attribute__((address_space(4)))*)p.tile_order;
     while (k < tiles_c) {
       const int t = order ? (int)order[c + k * nc] : c + k * nc;
-      const int row = t / p.n_tiles_x;
-      // the tile's time as -start + end in its cost word. Cost records are kept to the STATS
-      // instantiations (run_render picks one for a launch that records them): in the timed kernel
-      // the record costs C4 six more spilled VGPRs and 2.5% (A/B r4h)
-      if (STATS && p.tile_cost && lane == 0) p.tile_cost[t] = 0u - (uint32_t)__builtin_amdgcn_s_memrealtime();
-      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false, lds_tab, true);
-      if (STATS && p.tile_cost && lane == 0) atomicAdd(p.tile_cost + t, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      // (an order entry outside the launch's tiles — a stale or foreign order buffer — renders nothing
+      // rather than writing outside the frame)
+      if ((unsigned)t < (unsigned)nt) {
+        const int row = t / p.n_tiles_x;
+        // the tile's time as -start + end in its cost word. Cost records are kept to the STATS
+        // instantiations (run_render picks one for a launch that records them): in the timed kernel
+        // the record costs C4 six more spilled VGPRs and 2.5% (A/B r4h)
+        if (STATS && p.tile_cost && lane == 0) p.tile_cost[t] = 0u - (uint32_t)__builtin_amdgcn_s_memrealtime();
+        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false,
+                                                              lds_tab, true);
+        if (STATS && p.tile_cost && lane == 0) atomicAdd(p.tile_cost + t, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      }
       v = __builtin_amdgcn_readfirstlane(nxt);
       k = waves_c + v;
       if (k < tiles_c && lane == 0) nxt = atomicAdd(ctr, 1u);
@@ -1993,6 +2029,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
   int bx = blockIdx.x, by = gridDim.y - 1 - blockIdx.y, tb = blockIdx.y * gridDim.x + blockIdx.x;
   if (p.tile_order) {
     tb = (int)((const uint32_t __attribute__((address_space(4)))*)p.tile_order)[tb];
+    if ((unsigned)tb >= gridDim.x * gridDim.y) return;  // (block-uniform: a stale order renders nothing)
     bx = tb % gridDim.x;
     by = gridDim.y - 1 - tb / gridDim.x;
   }
@@ -2793,7 +2830,11 @@ int rtx_render_camera_sched(const double* scene, int n_spheres, int width, int h
   p.tile_order = tile_order;  // rtx_sched_tiles units of this launch (the first pass: mode 0, one frame)
   p.tile_cost = tile_cost;
   p.reserve = (int)((flags >> RTX_F_RESERVE_SHIFT) & 0xFFFu);
-  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream, (flags & RTX_F_NO_GENERAL) != 0);
+  // a launch with counters or cost records runs the STATS kernels, which have no texturing build:
+  // they defer image-textured hits, so the general kernel must follow whatever the caller learnt
+  // from the texturing build's deferral count
+  const bool no_general = (flags & RTX_F_NO_GENERAL) && !(p.images && (stats || tile_cost));
+  return run_render(p, workspace, workspace_bytes, (hipStream_t)stream, no_general);
 }
 
 int rtx_render_camera(const double* scene, int n_spheres, int width, int height, int row_block, int n_parts,

@@ -80,12 +80,17 @@ struct Tiles {
   int device;
   bool loop;  // RTX_TILES_LOOPBACK: a one-rank plan whose tile still goes through RCCL (send to itself)
   bool rows;  // RTX_TILES_ROWS: each row block travels on its own and lands in the frame (no assembly)
+  bool timed;  // RTX_TILES_TIMED: timing events around each slot's gather and assembly (rtx_tiles_timing)
   unsigned reserve;  // RTX_F_RESERVE bits passed to every render (plans that gather)
   hipStream_t cs;  // collective + assembly stream
   void* send[RTX_TILES_MAX_SLOTS];
   void* recv[RTX_TILES_MAX_SLOTS];
   hipEvent_t rendered[RTX_TILES_MAX_SLOTS];
   hipEvent_t done[RTX_TILES_MAX_SLOTS];
+  // RTX_TILES_TIMED, on the plan's stream: g0 when the gather may start (this rank's tile rendered,
+  // the slot's previous frame gone), g1 when the group's transfers are complete, a1 after the
+  // root's assembly (or the root's own row blocks under RTX_TILES_ROWS)
+  hipEvent_t g0[RTX_TILES_MAX_SLOTS], g1[RTX_TILES_MAX_SLOTS], a1[RTX_TILES_MAX_SLOTS];
   bool used[RTX_TILES_MAX_SLOTS];
 };
 
@@ -130,8 +135,8 @@ int gather_rows(Tiles* t, int slot, bool root, uint8_t* frame) {
   const ncclResult_t r2 = g_rccl.group_end();
   if (r != ncclSuccess) return nccl_err(root ? "ncclRecv" : "ncclSend", r);
   if (r2 != ncclSuccess) return nccl_err("ncclGroupEnd", r2);
-  hipError_t e = hipSuccess;
-  if (root && !t->loop) {  // the root's own blocks: rows (j P + root) rb .. + rb of the frame
+  hipError_t e = t->timed ? hipEventRecord(t->g1[slot], t->cs) : hipSuccess;
+  if (e == hipSuccess && root && !t->loop) {  // the root's own blocks: rows (j P + root) rb .. + rb of the frame
     const int n = t->local_rows, full = n / rb, tail = n % rb;
     const uint8_t* own = (const uint8_t*)t->recv[slot];
     uint8_t* dst0 = frame + (int64_t)t->root * rb * rowb;
@@ -142,6 +147,7 @@ int gather_rows(Tiles* t, int slot, bool root, uint8_t* frame) {
       e = hipMemcpyAsync(dst0 + (int64_t)full * P * rb * rowb, own + (int64_t)full * rb * rowb, (size_t)(tail * rowb),
                          hipMemcpyDeviceToDevice, t->cs);
   }
+  if (e == hipSuccess && t->timed) e = hipEventRecord(t->a1[slot], t->cs);
   if (e == hipSuccess) e = hipEventRecord(t->done[slot], t->cs);
   if (e != hipSuccess) return err(RTX_E_LAUNCH, "gather_rows: %s", hipGetErrorString(e));
   return RTX_OK;
@@ -222,7 +228,7 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   if (width <= 0 || height <= 0 || row_block <= 0) return err(RTX_E_ARG, "bad frame/tile geometry%s", "");
   if (out_kind < 0 || out_kind > 2) return err(RTX_E_ARG, "bad out_kind%s %lld", "", out_kind);
   if (slots < 1 || slots > RTX_TILES_MAX_SLOTS) return err(RTX_E_ARG, "bad slot count%s (%lld)", "", slots);
-  if (flags & ~(unsigned)(RTX_TILES_LOOPBACK | RTX_TILES_ROWS | RTX_F_RESERVE(0xFFF)))
+  if (flags & ~(unsigned)(RTX_TILES_LOOPBACK | RTX_TILES_ROWS | RTX_TILES_TIMED | RTX_F_RESERVE(0xFFF)))
     return err(RTX_E_ARG, "unknown flags%s (%lld)", "", (long long)flags);
   const bool loop = world == 1 && (flags & RTX_TILES_LOOPBACK);
   const bool rows = (flags & RTX_TILES_ROWS) && (world > 1 || loop);
@@ -268,6 +274,7 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
   t->local_rows = local_rows(height, row_block, np, t->first, t->my_run);
   t->loop = loop;
   t->rows = rows;
+  t->timed = (flags & RTX_TILES_TIMED) && (world > 1 || loop);
   t->reserve = (world > 1 || loop) ? (flags & RTX_F_RESERVE(0xFFF)) : 0u;
   (void)hipGetDevice(&t->device);
   hipError_t e = hipStreamCreateWithFlags(&t->cs, hipStreamNonBlocking);
@@ -276,6 +283,11 @@ int rtx_tiles_create(void* comm, int world, int rank, int root, int width, int h
     t->recv[s] = recv ? recv[s] : nullptr;
     e = hipEventCreateWithFlags(&t->rendered[s], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->done[s], hipEventDisableTiming);
+    if (t->timed) {
+      if (e == hipSuccess) e = hipEventCreate(&t->g0[s]);
+      if (e == hipSuccess) e = hipEventCreate(&t->g1[s]);
+      if (e == hipSuccess) e = hipEventCreate(&t->a1[s]);
+    }
   }
   if (e != hipSuccess) {
     rtx_tiles_destroy(t);
@@ -315,6 +327,7 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
   if (single) return RTX_OK;
   hipError_t e = hipEventRecord(t->rendered[slot], s);
   if (e == hipSuccess) e = hipStreamWaitEvent(t->cs, t->rendered[slot], 0);
+  if (e == hipSuccess && t->timed) e = hipEventRecord(t->g0[slot], t->cs);
   if (e != hipSuccess) return err(RTX_E_LAUNCH, "event: %s", hipGetErrorString(e));
   if (t->rows) return gather_rows(t, slot, root, (uint8_t*)frame);
   if (ncclResult_t r = g_rccl.group_start()) return nccl_err("ncclGroupStart", r);
@@ -334,12 +347,29 @@ int rtx_tiles_submit(void* plan, int slot, const double* scene, int n_spheres, i
   const ncclResult_t r2 = g_rccl.group_end();
   if (r != ncclSuccess) return nccl_err(root ? "ncclRecv" : "ncclSend", r);
   if (r2 != ncclSuccess) return nccl_err("ncclGroupEnd", r2);
+  if (t->timed && (e = hipEventRecord(t->g1[slot], t->cs)))
+    return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
   if (root) {
     if (int rc = rtx_assemble_runs(t->recv[slot], t->part_bytes, t->world, t->root_run, t->run, t->width, t->height,
                                    t->row_block, t->out_kind, frame, t->cs))
       return rc;
   }
+  if (t->timed && (e = hipEventRecord(t->a1[slot], t->cs)))
+    return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
   if ((e = hipEventRecord(t->done[slot], t->cs))) return err(RTX_E_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
+  return RTX_OK;
+}
+
+int rtx_tiles_timing(void* plan, int slot, float* gather_ms, float* assemble_ms) {
+  Tiles* t = (Tiles*)plan;
+  if (!t || !gather_ms || !assemble_ms) return err(RTX_E_ARG, "null argument%s", "");
+  if (slot < 0 || slot >= t->slots) return err(RTX_E_ARG, "bad slot%s (%lld)", "", slot);
+  if (!t->timed) return err(RTX_E_ARG, "the plan was not created with RTX_TILES_TIMED (or does not gather)%s", "");
+  if (!t->used[slot]) return err(RTX_E_ARG, "slot%s %lld has carried no frame", "", slot);
+  hipError_t e = hipEventSynchronize(t->a1[slot]);
+  if (e == hipSuccess) e = hipEventElapsedTime(gather_ms, t->g0[slot], t->g1[slot]);
+  if (e == hipSuccess) e = hipEventElapsedTime(assemble_ms, t->g1[slot], t->a1[slot]);
+  if (e != hipSuccess) return err(RTX_E_LAUNCH, "rtx_tiles_timing: %s", hipGetErrorString(e));
   return RTX_OK;
 }
 
@@ -361,6 +391,8 @@ int rtx_tiles_destroy(void* plan) {
   for (int s = 0; s < t->slots; ++s) {
     if (t->rendered[s]) (void)hipEventDestroy(t->rendered[s]);
     if (t->done[s]) (void)hipEventDestroy(t->done[s]);
+    for (hipEvent_t ev : {t->g0[s], t->g1[s], t->a1[s]})
+      if (ev) (void)hipEventDestroy(ev);
   }
   if (t->cs) (void)hipStreamDestroy(t->cs);
   delete t;

@@ -49,6 +49,15 @@ COMM_RESERVE_BLOCKS = 64
 ROOT_SHARES = {2: (8, 9), 3: (3, 4), 4: (3, 4), 5: (2, 3), 6: (2, 3), 7: (1, 2), 8: (1, 2)}
 
 
+def default_shares(world: int, dst: int = 0, rows: bool = False) -> tuple:
+    """(root_run, run) a TileGather takes unless told otherwise: ROOT_SHARES with the root at rank 0;
+    even shares for a root elsewhere, and for RTX_TILES_ROWS (each row block of a part travels on
+    its own into the frame; the native plan takes runs of one part only)."""
+    if rows or dst != 0:
+        return (1, 1)
+    return ROOT_SHARES.get(int(world), (1, 1))
+
+
 # RCCL communicators of the native path, one per (process group, rank, device): creating one costs
 # a rendezvous, so TileGathers of the same group share it for the life of the process
 _COMMS: dict = {}
@@ -93,7 +102,7 @@ class TileGather:
     def __init__(self, renderer, width: int, height: int, *, group=None, row_block: int = 8, dst: int = 0,
                  out: str | None = None, slots: int = 2, native: bool | None = None,
                  persistent_frames: bool = False, loopback: bool = False, comm_reserve: int | None = None,
-                 rows: bool | None = None, shares: tuple | None = None) -> None:
+                 rows: bool | None = None, shares: tuple | None = None, timed: bool = False) -> None:
         """``native``: drive each frame through rtx_tiles_submit (default: under RCCL with a
         renderer that has ``submit_tiles``); False keeps torch.distributed.gather. ``persistent_frames``
         (native root): assemble every frame of a slot into one buffer kept by the slot, so a frame
@@ -107,8 +116,10 @@ class TileGather:
         operation (one GPU, C4 loopback: 5,480 us per step with row blocks of 8 rows, 2,837 with 32,
         against 2,190 gathered whole and assembled). ``shares`` = (root_run, run): rank 0 renders
         root_run parts and every other rank run parts of a root_run + (world - 1) run interleave
-        (tiling.runs); default ROOT_SHARES by world size (the root also receives and assembles every
-        frame, so it takes a smaller share; the root must then be rank 0)."""
+        (tiling.runs); default ``default_shares``: ROOT_SHARES by world size (the root also receives
+        and assembles every frame, so it takes a smaller share; the root must then be rank 0), even
+        shares with ``rows`` (which moves parts of one run each). ``timed`` (native plans that
+        gather): timing events around every gather (RTX_TILES_TIMED), read by ``timing(slot)``."""
         import torch.distributed as dist
 
         self._dist = dist
@@ -124,10 +135,12 @@ class TileGather:
         dtype = torch.uint8 if self.out == "u8" else getattr(renderer, "color_dtype", torch.float64)
         self.device = torch.device(getattr(renderer, "device", "cpu"))
         if shares is None:
-            shares = ROOT_SHARES.get(self.world, (1, 1)) if self.dst == 0 else (1, 1)
+            shares = default_shares(self.world, self.dst, bool(rows) and self.out == "u8")
         self.root_run, self.run = int(shares[0]), int(shares[1])
         if self.root_run != self.run and self.dst != 0:
             raise ValueError("unequal shares need the root at rank 0")
+        if rows and self.out == "u8" and (self.root_run, self.run) != (1, 1):
+            raise ValueError("rows=True (RTX_TILES_ROWS) moves parts of one run each: shares must be (1, 1)")
         self.n_parts, runs = tiling.runs(self.world, self.root_run, self.run)
         self.first, self.my_run = runs[self.rank]
         self.shape = tiling.tile_shape(self.H, self.W, self.rb, self.n_parts, self.first, self.out, self.my_run)
@@ -141,7 +154,7 @@ class TileGather:
         if native:
             self._init_native(dtype, plen, slots, persistent_frames, loopback and self.world == 1,
                               COMM_RESERVE_BLOCKS if comm_reserve is None else int(comm_reserve),
-                              bool(rows) and self.out == "u8")
+                              bool(rows) and self.out == "u8", bool(timed))
             return
         # zero-filled once: the padding beyond a short part's tile is sent but never read
         self.send = [torch.zeros(plen, dtype=dtype, device=self.device) for _ in range(slots)]
@@ -152,7 +165,7 @@ class TileGather:
         self._recv_lists = [list(b.unbind(0)) for b in self.recv] if self.recv is not None else None
         self._views = [b[:self.n].view(self.shape) for b in self.send]
 
-    def _init_native(self, dtype, plen, slots, persistent_frames, loop, reserve, rows) -> None:
+    def _init_native(self, dtype, plen, slots, persistent_frames, loop, reserve, rows, timed=False) -> None:
         import ctypes
 
         from python_ray_tracer_amd.infrastructure.hip import _lib as L
@@ -166,6 +179,8 @@ class TileGather:
                      if not root or loop else [])
         gathers = self.world > 1 or loop
         self.rows = rows and gathers
+        self.timed = timed and gathers
+        self.part_bytes = plen * torch.empty((), dtype=dtype).element_size()
         # RTX_TILES_ROWS: the root keeps only its own tile (the peers' blocks land in the frame)
         self.recv = ([torch.zeros((1 if self.rows else self.world, plen), dtype=dtype, device=self.device)
                       for _ in range(slots)] if root and gathers else None)
@@ -184,6 +199,7 @@ class TileGather:
                                                slots, send, recv, plen * torch.empty((), dtype=dtype).element_size(),
                                                self.root_run, self.run,
                                                (L.TILES_LOOPBACK if loop else 0) | (L.TILES_ROWS if self.rows else 0)
+                                               | (L.TILES_TIMED if self.timed else 0)
                                                | ((reserve & 0xFFF) << L.F_RESERVE_SHIFT),
                                                ctypes.byref(plan)),
                     "rtx_tiles_create")
@@ -238,6 +254,25 @@ class TileGather:
         if hasattr(self.r, "assemble_rows"):  # HipRenderer: the device un-permute
             return self.r.assemble_rows(tiles, self.W, self.H, self.rb, self.out, self.root_run, self.run)
         return tiling.assemble(tiles, self.H, self.W, self.rb, self.out, self.root_run, self.run)
+
+    def timing(self, slot: int = 0) -> dict:
+        """The measured gather of slot ``slot``'s latest frame on this rank (a ``timed`` native plan
+        that gathers; rtx_tiles_timing, synchronising): ``gather_ms`` from this rank's tile rendered
+        to its RCCL group complete (a peer: its part delivered to the root; the root: every peer's
+        part received), ``assemble_ms`` the root's assembly, ``bytes`` this rank's RCCL traffic per
+        frame (a peer sends part_bytes; the root receives (world - 1) part_bytes)."""
+        import ctypes
+
+        if self.plan is None or not getattr(self, "timed", False):
+            raise RuntimeError("timing() needs a native plan that gathers, created with timed=True")
+        g, a = ctypes.c_float(), ctypes.c_float()
+        with torch.cuda.device(self.device):
+            self._L.check(self._lib.rtx_tiles_timing(self.plan, int(slot), ctypes.byref(g), ctypes.byref(a)),
+                          "rtx_tiles_timing")
+        peers = max(self.world - 1, 1)
+        nbytes = self.part_bytes * (peers if self.rank == self.dst else 1)
+        return {"gather_ms": float(g.value), "assemble_ms": float(a.value), "bytes": int(nbytes),
+                "part_bytes": int(self.part_bytes)}
 
     def render(self, scene):
         """One frame, synchronous in program order: submit + finish on slot 0."""

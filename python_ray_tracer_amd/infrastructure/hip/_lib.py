@@ -95,11 +95,13 @@ EXPORTS = (
     "rtx_tiles_submit",
     "rtx_tiles_finish",
     "rtx_tiles_destroy",
+    "rtx_tiles_timing",
 )
 
 TILES_MAX_SLOTS = 4
 TILES_LOOPBACK = 1  # rtx_tiles_create flags
 TILES_ROWS = 2
+TILES_TIMED = 4
 UNIQUE_ID_BYTES = 128  # ncclUniqueId
 
 _c_void_p = ctypes.c_void_p
@@ -144,6 +146,7 @@ _SIGS = {
                                        _c_void_p]),
     "rtx_tiles_finish": (_i32, [_c_void_p, _i32, _c_void_p]),
     "rtx_tiles_destroy": (_i32, [_c_void_p]),
+    "rtx_tiles_timing": (_i32, [_c_void_p, _i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
 }
 
 _lib = None

@@ -235,6 +235,7 @@ class HipRenderer(Renderer):
         # False defers those pixels to the general kernel (same colours)
         self.fast_textures = bool(fast_textures)
         self._ws = None
+        self._graph_pins: list = []  # tensors a captured launch points at (_tile_launch)
         self.stats_buffer = torch.zeros(L.S_WORDS, dtype=torch.int64, device=self.device) if collect_stats else None
 
     # ---------------------------------------------------------------- plumbing
@@ -404,6 +405,11 @@ class HipRenderer(Renderer):
                 flags |= gflags
             if self.learn_tile_order:
                 order, cost = self._sched_plan(key, int(scene.camera.width), rows, n_spheres)
+        if torch.cuda.is_current_stream_capturing():
+            # a captured launch keeps raw pointers to the blob, the workspace and the learnt order:
+            # pin them for the renderer's life, so that a cache eviction (scene cache, workspace
+            # growth, the 64-key order cache) cannot free memory a graph replay reads
+            self._graph_pins.extend(t for t in (blob, ws, order) if t is not None)
         return blob, n_spheres, rows, ws, flags, probe, key, order, cost
 
     def _sched_plan(self, key, width, rows, n_spheres):

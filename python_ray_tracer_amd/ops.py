@@ -10,9 +10,10 @@ workspace, like a TORCH_CHECK; each runs under a device guard of its input's dev
 that device's current HIP stream and returns a new tensor):
 
 * ``rt::render_tile(scene, n_spheres, width, height, row_block, n_parts, part, max_bounces,
-  out_kind, workspace, stats=None, check=True)`` — get_ray_directions + raytrace_scene fused
-  (base.py:91-141) for one interleaved row tile; out_kind 0 = float32 [3, n], 1 = float64 [3, n],
-  2 = uint8 [rows, W, 3].
+  out_kind, workspace, stats=None, check=True, part_run=1)`` — get_ray_directions + raytrace_scene
+  fused (base.py:91-141) for one interleaved row tile, or the run of ``part_run`` parts from
+  ``part`` (a rank's weighted share, distributed.ROOT_SHARES); out_kind 0 = float32 [3, n],
+  1 = float64 [3, n], 2 = uint8 [rows, W, 3].
 * ``rt::render_frames(scenes, n_spheres, width, height, max_bounces, out_kind, workspace,
   stats=None, check=True)`` — F whole frames in one launch (``scenes``: [F, L], one packed blob per
   row); [F, 3, W*H] colour or [F, H, W, 3] uint8 (HipRenderer.render_batch).
@@ -23,7 +24,9 @@ that device's current HIP stream and returns a new tensor):
   ``t`` [n] (shader.py:63-112; HipShader.create).
 * ``rt::intersect(sphere, origins, dirs)`` — NumpySphere.intersect (shape.py:28-51).
 * ``rt::quantize_u8(color)`` — save_image's quantisation (base.py:143-151) -> [n, 3] uint8.
-* ``rt::assemble_rows(tiles, width, height, row_block, out_kind)`` — the multi-GPU row un-permute.
+* ``rt::assemble_rows(tiles, width, height, row_block, out_kind, root_run=1, run=1)`` — the
+  multi-GPU row un-permute of ``tiles`` [ranks, part_len]: rank 0's run of ``root_run`` parts, each
+  other rank's run of ``run`` (tiling.runs; 1, 1 = one part per rank).
 * ``rt::status(workspace)`` — reads and clears the sticky RTX_ST_* flags (1 stack overflow,
   2 deferred-list overflow, 4 bad scene); synchronises.
 * ``rt::workspace_bytes(n_rays, max_bounces)``.

@@ -58,7 +58,20 @@ def _worker(rank, world, port, spec, B, row_block, outdir):
         tg.submit(scene, 0)
         tg.submit(orbit, 1)
         f0, f1 = tg.finish(0), tg.finish(1)
+        # rows=True (RTX_TILES_ROWS on a native plan) takes even shares: the native plan moves parts
+        # of one run each; explicit unequal shares with rows are refused up front
+        W, H = spec["camera"]["width"], spec["camera"]["height"]
+        tgr = TileGather(r, W, H, row_block=row_block, out="u8", rows=True)
+        assert (tgr.root_run, tgr.run) == (1, 1)
+        f_rows = tgr.render(scene)
+        try:
+            TileGather(r, W, H, row_block=row_block, out="u8", rows=True, shares=(1, 2))
+        except ValueError:
+            pass
+        else:
+            raise AssertionError("unequal shares with rows=True must be refused")
         if rank == 0:
+            np.save(os.path.join(outdir, "rows_u8.npy"), f_rows.numpy())
             np.save(os.path.join(outdir, "frame.npy"), frame.numpy())
             np.save(os.path.join(outdir, "frame_u8.npy"), frame_u8.numpy())
             np.save(os.path.join(outdir, "pipe0.npy"), f0.numpy())
@@ -104,6 +117,7 @@ def test_row_tiles_gather_equals_single_frame(world, row_block):
         want = O.render(O.scene_from_spec(spec), B)
         assert np.array_equal(frame, want)
         assert np.array_equal(frame_u8, O.to_uint8(want, 40, 27))
+        assert np.array_equal(np.load(os.path.join(d, "rows_u8.npy")), O.to_uint8(want, 40, 27))
         assert np.array_equal(np.load(os.path.join(d, "pipe0.npy")), want)
         orbit = O.render(O.scene_from_spec(scenes.with_camera(spec, scenes.orbit_position(3, 8))), B)
         assert np.array_equal(np.load(os.path.join(d, "pipe1.npy")), orbit)
@@ -111,6 +125,20 @@ def test_row_tiles_gather_equals_single_frame(world, row_block):
         assert set().union(*shards) == set(range(8))
         for r in range(world):
             assert shards[r] == {k for k in range(8) if k % world == r}
+
+
+def test_default_shares():
+    """TileGather's default shares: ROOT_SHARES with the root at rank 0, even shares for a root
+    elsewhere and for row-block gathers (RTX_TILES_ROWS takes runs of one part: ADVICE r4)."""
+    from python_ray_tracer_amd.distributed import ROOT_SHARES, default_shares
+
+    assert default_shares(1) == (1, 1)
+    for w in range(2, 9):
+        assert default_shares(w) == ROOT_SHARES[w]
+        assert default_shares(w, rows=True) == (1, 1)
+        assert default_shares(w, dst=1) == (1, 1)
+        n_parts, runs = tiling.runs(w, *default_shares(w))
+        assert runs[0][0] == 0 and sum(k for _, k in runs) == n_parts
 
 
 def test_row_tiled_cpu_baseline_runs():

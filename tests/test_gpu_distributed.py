@@ -41,6 +41,32 @@ def test_two_ranks_share_gpu_gather_equals_single_frame(tmp_path):
     assert "False" not in logs["rank0.txt"] and "png_u8" in logs["rank0.txt"], logs
 
 
+def test_native_tiles_world_gt1_through_rccl_stub():
+    """The native plan's world > 1 code (rtx_tiles.hip: the root's per-peer receives into
+    recv + p * part_bytes while it renders its own share, the peers' sends, rtx_assemble_runs over
+    the weighted shares 8:9 / 3:4 / 1:2, gather_rows for RTX_TILES_ROWS) on the box's one GPU: N ranks
+    as threads of one fresh process, each with its own renderer, stream and plan, RCCL bound to the
+    test-only stub (tests/stub_rccl.cpp: sends matched to receives in posting order, device copies on
+    the receiver's stream). Two slots in flight; u8 and f32; capped and unbounded. The root's frames
+    equal the single-GPU render bit for bit and the stub's log holds exactly the operations the plan's
+    layout implies (tests/stub_tiles_worker.py)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+
+    stub = REPO / "tests" / "libstub_rccl.so"
+    assert stub.exists(), "build() compiles tests/libstub_rccl.so"
+    p = subprocess.run([sys.executable, "-u", str(REPO / "tests" / "stub_tiles_worker.py")], cwd=str(REPO),
+                       capture_output=True, text=True, timeout=115)
+    lines = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert p.returncode == 0, (p.returncode, lines, p.stderr[-3000:])
+    cases = {c["case"]: c for c in lines if "case" in c}
+    assert {"n2_8to9_f32", "n4_3to4_u8", "n8_1to2_u8", "n8_1to2_f32", "n4_rows_u8",
+            "n3_3to4_f32_unbounded"} <= set(cases), cases
+    for c in cases.values():
+        assert c["ok"] and all(c["frames_equal"]) and c["log_matches"], c
+
+
 def test_nccl_two_slot_pipeline_equals_single_frames():
     """TileGather under nccl (a one-rank RCCL group on the box's one GPU): orbit frames pushed
     through the two-slot pipeline of bench.py's tiles mode (submit k, finish k-1; the gather runs on
@@ -136,5 +162,47 @@ def test_native_tiles_loopback_and_graph_replay():
             torch.cuda.synchronize()
             assert torch.equal(buf, want[3])
             assert torch.equal(tgd.frames[0], want[3])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_tiles_loopback_plan_in_a_graph():
+    """A gathering plan captured into a HIP graph: the loopback plan's RCCL send/receive (on the
+    plan's stream, forked from and joined back to the capturing stream by the plan's events) and the
+    assembly sit inside the graph; replays give the eager frame bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.distributed as dist
+
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.distributed import TileGather
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        sc = scenes.build_scene(scenes.random_spec(40, 6, 96, 61))
+        r = HipRenderer(max_bounces=3, color_dtype=torch.float32, device=dev)
+        want = r.render_tile(sc, out="u8").clone()
+        for rows in (False, True):
+            tg = TileGather(r, 96, 61, row_block=8, out="u8", slots=1, loopback=True, rows=rows,
+                            persistent_frames=True)
+            tg.submit(sc, 0)  # eager first: the learnt order, the probe, RCCL's own set-up
+            assert torch.equal(tg.finish(0), want)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    tg.submit(sc, 0)
+                    tg.finish(0)
+            torch.cuda.synchronize()
+            for _ in range(3):
+                tg.frames[0].zero_()
+                g.replay()
+                torch.cuda.synchronize()
+                assert torch.equal(tg.frames[0], want), rows
     finally:
         dist.destroy_process_group()

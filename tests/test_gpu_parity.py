@@ -611,6 +611,15 @@ def test_fast_kernel_texturing_build(hip, B):
         fast = hip.HipRenderer(max_bounces=B, color_dtype=torch.float32)
         slow = hip.HipRenderer(max_bounces=B, color_dtype=torch.float32, fast_textures=False)
         assert torch.equal(fast.render(scene).data, slow.render(scene).data), (B, S)
+        # the texturing build against the oracle directly (not only against the general kernel):
+        # float64 colour within 1e-12, up to 1 pixel in 10^4 on a texel edge (atan2 / asin, as in
+        # test_image_textured_spheres); the first render learns the order, the second is the timed path
+        f64 = hip.HipRenderer(max_bounces=B, color_dtype=torch.float64)
+        want = O.render(O.scene_from_spec(spec), B)
+        for _ in range(2):
+            got = f64.render(scene).data.cpu().numpy()
+            bad = (np.abs(got - want) > ATOL).any(axis=0)
+            assert bad.sum() <= max(1, got.shape[1] // 10000), (B, S, int(bad.sum()))
         for P, part in ((3, 1), (4, 3)):
             assert torch.equal(fast.render_tile(scene, 8, P, part, out="u8"),
                                slow.render_tile(scene, 8, P, part, out="u8")), (B, S, P)

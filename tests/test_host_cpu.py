@@ -98,6 +98,7 @@ def test_sched_and_tiles_entry_points_validate_on_host():
     lib = L.load()
     text = (REPO / "include" / "rtx_hip.h").read_text()
     for name, val in (("RTX_TILES_LOOPBACK", L.TILES_LOOPBACK), ("RTX_TILES_ROWS", L.TILES_ROWS),
+                      ("RTX_TILES_TIMED", L.TILES_TIMED),
                       ("RTX_F_RESERVE_SHIFT", L.F_RESERVE_SHIFT), ("RTX_F_IMAGES", L.F_IMAGES), ("RTX_TILES_MAX_SLOTS", L.TILES_MAX_SLOTS)):
         assert int(re.search(rf"#define\s+{name}\s+(\d+)", text).group(1)) == val, name
     n = ctypes.c_int64()
@@ -134,6 +135,8 @@ def test_sched_and_tiles_entry_points_validate_on_host():
     assert plan.value is None
     assert lib.rtx_tiles_submit(None, 0, None, 3, 3, None, 0, 0, None, None, None, None, None) == -1
     assert lib.rtx_tiles_destroy(None) == 0
+    f1, f2 = ctypes.c_float(), ctypes.c_float()
+    assert lib.rtx_tiles_timing(None, 0, ctypes.byref(f1), ctypes.byref(f2)) == -1
 
 
 def test_pack_matches_reference_expressions():
@@ -408,6 +411,19 @@ def test_torch_ops_schema_and_fake_kernels():
     assert torch.ops.rt.intersect(blob[:8], o, d).shape == (11,)
     assert torch.ops.rt.quantize_u8(d).shape == (11, 3)
     assert torch.ops.rt.assemble_rows(torch.empty(2, 64, dtype=torch.uint8, **meta), 4, 4, 1, 2).shape == (4, 4, 3)
+    # weighted shares (round 5): a run of parts per render, and the un-permute of unequal runs
+    assert "int part_run=1" in str(torch.ops.rt.render_tile.default._schema)
+    assert "int root_run=1, int run=1" in str(torch.ops.rt.assemble_rows.default._schema)
+    for part, run in ((0, 1), (1, 2), (3, 2)):  # 17 rows in blocks of 2 over 5 parts, runs from `part`
+        want = tiling.n_local_rows(17, 2, 5, part, run)
+        got = torch.ops.rt.render_tile(blob, 3, 20, 17, 2, 5, part, 3, 2, ws, part_run=run)
+        assert got.shape == (want, 20, 3), (part, run)
+    with pytest.raises(RuntimeError, match="geometry"):
+        torch.ops.rt.render_tile(blob, 3, 20, 17, 2, 5, 4, 3, 2, ws, part_run=2)  # past the interleave
+    tiles = torch.empty(3, 64 * 9, dtype=torch.uint8, **meta)
+    assert torch.ops.rt.assemble_rows(tiles, 8, 16, 2, 2, root_run=1, run=2).shape == (16, 8, 3)
+    with pytest.raises(RuntimeError, match="run"):
+        torch.ops.rt.assemble_rows(tiles, 8, 16, 2, 2, root_run=0, run=2)
 
 
 def test_ops_refuse_a_variant_library():

@@ -48,7 +48,7 @@ def main():
     # default: the library's two units (the small-scene kernels live in rtx_small.hip, built with
     # _build.SMALL_FLAGS); each source is a column
     srcs = [Path(s) for s in sys.argv[1:]] or [_build.SRC, _build.SMALL_SRC]
-    procs = [subprocess.Popen([_build.hipcc(), *FLAGS, *(_build.SMALL_FLAGS if s.name == _build.SMALL_SRC.name else []),
+    procs = [subprocess.Popen([_build.hipcc(), *FLAGS, *(_build.SMALL_FLAGS if "small" in s.name else []),
                                "--cuda-device-only", "-c",
                                "-Rpass-analysis=kernel-resource-usage", "-o", "/dev/null", str(s)],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for s in srcs]
