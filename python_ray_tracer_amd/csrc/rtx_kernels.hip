@@ -87,9 +87,12 @@ constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD oth
 // bar), and no level's inputs live in LDS slots or registers across the chain: C4's B = 5 kernel
 // kept three levels in a register shift (27 VGPRs, the bulk of its 41 spilled) beside two LDS slots.
 // The DEEP kernels keep the backward fold (their resume records carry the levels' inputs).
+// A/B r5c (one box, tools/ab.py, frames identical): C2 55.20 -> 52.94 us (-4.1%), C4 2,055 -> 1,874 us
+// (-8.8%: 41 spilled VGPRs -> 0), C3 273.1 -> 265.7 us (-2.7%, at 5 waves/SIMD; 283.9 at 4)
 constexpr bool kForwardFold = true;
-constexpr int kFwdWaves = 4;        // waves/SIMD of the forward-fold kernels with a culling tree
-constexpr int kFwdWavesSmall = 5;   // ... and of their TREE = false instantiations
+constexpr int kFwdWavesPersist = 4;  // waves/SIMD of the forward-fold persistent kernels (TP 2; C4: 5 waves 2,025 us)
+constexpr int kFwdWaves = 5;         // ... of the culled one-tile-per-block kernels (TP 1; C3: 4 waves 283.9 us)
+constexpr int kFwdWavesSmall = 5;    // ... and of the TREE = false kernels (TP 0; C2: 6 waves 56.0 us, spills)
 constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
                                      // 8-level instantiation spills, 3 defers too many pixels)
 constexpr int kCappedMax = RTX_FAST_MAX_BOUNCES;  // caps rendered entirely by k_render_fast<cap>
@@ -1937,7 +1940,7 @@ template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), 
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
                              (DEEP  ? kDeepWaves
                               : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
-                              : kForwardFold ? (TP ? kFwdWaves : kFwdWavesSmall)
+                              : kForwardFold ? (TP >= 2 ? kFwdWavesPersist : TP ? kFwdWaves : kFwdWavesSmall)
                                              : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   constexpr bool TREE = TP >= 1;
   // reflected-ray beams (wave_beam): scenes of kPersistMinSpheres and more, capped renders (A/B: C4

@@ -166,10 +166,11 @@ def test_native_tiles_loopback_and_graph_replay():
         dist.destroy_process_group()
 
 
-def test_native_tiles_loopback_plan_in_a_graph():
-    """A gathering plan captured into a HIP graph: the loopback plan's RCCL send/receive (on the
-    plan's stream, forked from and joined back to the capturing stream by the plan's events) and the
-    assembly sit inside the graph; replays give the eager frame bit for bit."""
+def test_gathering_plan_refuses_graph_capture(monkeypatch):
+    """RCCL send/recv captured into a HIP graph crashes capture_end on this image (session r5a:
+    segfault in torch.cuda.graph's capture_end for a loopback plan), so TileGather refuses to submit
+    a gathering plan under stream capture with a RuntimeError instead; a one-rank plan without RCCL
+    traffic still captures (test_native_tiles_loopback_and_graph_replay)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import torch.distributed as dist
@@ -185,24 +186,12 @@ def test_native_tiles_loopback_plan_in_a_graph():
         sc = scenes.build_scene(scenes.random_spec(40, 6, 96, 61))
         r = HipRenderer(max_bounces=3, color_dtype=torch.float32, device=dev)
         want = r.render_tile(sc, out="u8").clone()
-        for rows in (False, True):
-            tg = TileGather(r, 96, 61, row_block=8, out="u8", slots=1, loopback=True, rows=rows,
-                            persistent_frames=True)
-            tg.submit(sc, 0)  # eager first: the learnt order, the probe, RCCL's own set-up
-            assert torch.equal(tg.finish(0), want)
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream(dev)
-            s.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
-                    tg.submit(sc, 0)
-                    tg.finish(0)
-            torch.cuda.synchronize()
-            for _ in range(3):
-                tg.frames[0].zero_()
-                g.replay()
-                torch.cuda.synchronize()
-                assert torch.equal(tg.frames[0], want), rows
+        tg = TileGather(r, 96, 61, row_block=8, out="u8", slots=1, loopback=True, persistent_frames=True)
+        monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+        with pytest.raises(RuntimeError, match="cannot be captured"):
+            tg.submit(sc, 0)
+        monkeypatch.undo()
+        tg.submit(sc, 0)  # eagerly: fine
+        assert torch.equal(tg.finish(0), want)
     finally:
         dist.destroy_process_group()

@@ -246,4 +246,4 @@ def test_ops_accept_inference_tensors(env):
         for _ in range(2):
             assert torch.equal(torch.ops.rt.render_tile(blob, S, 40, 23, 1, 1, 0, 3, 0, ws), want)
         with pytest.raises(RuntimeError, match="holds 3 spheres"):
-            torch.ops.rt.render_tile(blob, S + 1, 40, 23, 1, 1, 0, 3, 0, ws)
+            torch.ops.rt.render_tile(blob, S - 1, 40, 23, 1, 1, 0, 3, 0, ws)

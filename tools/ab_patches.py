@@ -320,7 +320,45 @@ def block_plain(src: str) -> str:
                 "    atomicMax(p.tile_cost + tb, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_entry));\n", "")
 
 
-PATCHES = {f.__name__: f for f in (inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
+# ---------------------------------------------------------------------------------------------- round 5
+def nu_select(src: str) -> str:
+    """nearest_update by selects (no exec-mask branches): the same tmin / hit / tie."""
+    old = """  if (valid && t < tmin) {
+    tmin = t;
+    hit = s;
+    tie = false;
+  } else if (valid && t == tmin) {
+    tie = true;
+  }
+}"""
+    new = """  const bool lt = valid && t < tmin;
+  const bool eq = valid && t == tmin;
+  tie = lt ? false : (tie || eq);
+  hit = lt ? s : hit;
+  tmin = lt ? t : tmin;
+}"""
+    return _sub(src, old, new)
+
+
+def abl_noshadow_small(src: str) -> str:
+    """Ablation (wrong output): scenes below kTreeMinSpheres test no shadow ray (every hit lit)."""
+    return _sub(src, "    const int nshadow = nsph - (hs < nsph);\n    double tsh = FARAWAY;",
+                "    const int nshadow = 0;  // ablation\n    double tsh = FARAWAY;")
+
+
+def abl_nospec(src: str) -> str:
+    """Ablation (wrong output): the physical specular is not evaluated (0); V still is (iridescence)."""
+    return _sub(src, "    if (weighted) spec = specular(mh, g, nx, ny, nz, lx, ly, lz, vx, vy, vz);",
+                "    if (weighted) spec = 0.0;  // ablation")
+
+
+def abl_noirid(src: str) -> str:
+    """Ablation (wrong output): no thin-film iridescence term (nor V where only it needs V)."""
+    src = _sub(src, "  const bool need_irid = mh[RTX_M_IG] != 0.0;", "  const bool need_irid = false;  // ablation")
+    return _sub(src, "  if (igain != 0.0) {", "  if (false) {  // ablation")
+
+
+PATCHES = {f.__name__: f for f in (abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
                                    lv_together, self_triple, lv_triple, tile_trace, persist_plain, block_plain)}
 
 
