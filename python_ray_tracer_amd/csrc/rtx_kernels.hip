@@ -923,6 +923,9 @@ struct Hit {
 };
 
 // _calculate_physical_specular, shader.py:246-320, for unit-ish L (once normalised) and V.
+// Sums of non-negative terms here and in hit_color are fused multiply-adds (one rounding fewer,
+// within an ulp of the term; A/B r5e: C2 -1.6%, C2main -1.4%, C3 -1.2%, C4 -0.6%): none of them
+// decides anything, and none cancels, so the colour moves by at most a few ulp.
 template <typename M>
 __device__ __forceinline__ double specular(const M* mh, double g, double nx, double ny, double nz, double lx,
                                            double ly, double lz, double vx, double vy, double vz) {
@@ -946,20 +949,21 @@ __device__ __forceinline__ double specular(const M* mh, double g, double nx, dou
   const double NdotH = clip01(dot3(nx, ny, nz, Hx, Hy, Hz));  // :284
   const double VdotH = clip01(dot3(Vx, Vy, Vz, Hx, Hy, Hz));  // :285
   const double NdotL = clip01(dot3(nx, ny, nz, Lx, Ly, Lz));  // :287
-  const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291
+  const double F = __builtin_fma(mh[RTX_M_1MF0], pow5(1.0 - VdotH), mh[RTX_M_F0]);  // :291
   const double a2 = mh[RTX_M_A2];
-  const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295
-  const double Dd = RTX_PI * ((denom * denom) + 1e-8);  // :296
+  const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295 (not fused: the sum cancels
+  // to ~a^2 near the highlight's peak, and D amplifies the product's rounding by ~1/a^2)
+  const double Dd = RTX_PI * __builtin_fma(denom, denom, 1e-8);  // :296
   const double oma2 = mh[RTX_M_1MA2];
-  const double dL = (NdotL + sqrt_shade(a2 + oma2 * (NdotL * NdotL))) + 1e-8;  // :299-301
-  const double dV = (NdotV + sqrt_shade(a2 + oma2 * (NdotV * NdotV))) + 1e-8;
+  const double dL = (NdotL + sqrt_shade(__builtin_fma(oma2, NdotL * NdotL, a2))) + 1e-8;  // :299-301
+  const double dV = (NdotV + sqrt_shade(__builtin_fma(oma2, NdotV * NdotV, a2))) + 1e-8;
   // G = G1L * G1V and spec_base = (F D G) / (4 N.V + 1e-8) with D = a2 / Dd: the four quotients
   // of :296-306 as two reciprocals (a few ulp, like the single quotients' Newton sequences; the
   // 1e-12 parity bar holds on every test and 8,600 random scenes)
   const double G = ((2.0 * NdotL) * (2.0 * NdotV)) * div_shade(1.0, dL * dV);  // :303
-  const double spec_base = ((F * a2) * G) * div_shade(1.0, Dd * ((4.0 * NdotV) + 1e-8));  // :306
+  const double spec_base = ((F * a2) * G) * div_shade(1.0, Dd * __builtin_fma(4.0, NdotV, 1e-8));  // :306
   const double glint = pow25(1.0 - NdotV) * NdotL;  // :310-312
-  const double sf = spec_base + g * glint;  // :315
+  const double sf = __builtin_fma(g, glint, spec_base);  // :315
   return (NdotV <= 0.0) ? 0.0 : sf;  // :318
 }
 
@@ -991,9 +995,9 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
   }
   const double dg = mh[RTX_M_DG];
   // ambient + diffuse (:86-88, :138-141), dome (:98, :244)
-  const double ar = (0.004 + ((tr * dli) * litf) * dg) + sc[RTX_H_DOMEC + 0] * di;
-  const double ag = (0.004 + ((tg * dli) * litf) * dg) + sc[RTX_H_DOMEC + 1] * di;
-  const double ab = (0.004 + ((tb * dli) * litf) * dg) + sc[RTX_H_DOMEC + 2] * di;
+  const double ar = __builtin_fma(sc[RTX_H_DOMEC + 0], di, __builtin_fma((tr * dli) * litf, dg, 0.004));
+  const double ag = __builtin_fma(sc[RTX_H_DOMEC + 1], di, __builtin_fma((tg * dli) * litf, dg, 0.004));
+  const double ab = __builtin_fma(sc[RTX_H_DOMEC + 2], di, __builtin_fma((tb * dli) * litf, dg, 0.004));
   // specular + reflection (:106)
   const double g = mh[RTX_M_G];
   const double xr = weighted ? (spec + Rr * 0.5) * g : 0.0;
@@ -1007,9 +1011,9 @@ __device__ __forceinline__ void hit_color(const M* mh, const cdouble* sc, double
     const double phase = ((af * RTX_PI) * mh[RTX_M_TFT]) * 10.0;  // :208
     const double ip = sin_ref(sc, phase);  // :211
     const double hs = mh[RTX_M_HS], omhs = mh[RTX_M_1MHS];
-    const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221
-    const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222
-    const double b = 0.5 + 0.5 * ip;  // :223
+    const double r = __builtin_fma(ip, hs, omhs * (1.0 - ip));  // :221
+    const double gg = __builtin_fma(ip, omhs, hs * (1.0 - ip));  // :222
+    const double b = __builtin_fma(0.5, ip, 0.5);  // :223
     const double w = mh[RTX_M_TFW];
     ir = (r * w) * igain;  // :229-232
     ig = (gg * w) * igain;
@@ -1796,9 +1800,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       double lr_, lg_, lb_;
       hit_color<IMG>(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
                      s.va, 0.0, 0.0, 0.0, lr_, lg_, lb_);
-      cr = cr + thr * lr_;
-      cg = cg + thr * lg_;
-      cb = cb + thr * lb_;
+      cr = __builtin_fma(thr, lr_, cr);
+      cg = __builtin_fma(thr, lg_, cg);
+      cb = __builtin_fma(thr, lb_, cb);
       if (!weighted || k >= B) break;
       thr = (thr * 0.5) * s.g;  // the reflection's weight, (R * 0.5) * g (shader.py:106)
     } else if (!weighted || k >= B || at_cap) {

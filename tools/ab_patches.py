@@ -358,7 +358,45 @@ def abl_noirid(src: str) -> str:
     return _sub(src, "  if (igain != 0.0) {", "  if (false) {  // ablation")
 
 
-PATCHES = {f.__name__: f for f in (abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
+def shade_fma(src: str) -> str:
+    """Multiply-adds of the shading-only arithmetic (specular, colour terms, iridescence, the forward
+    fold) as fused fmas: a few ulp of colour (no hit, shadow, checker or reflection decision reads
+    them), one rounding and one instruction fewer each."""
+    subs = [
+        ("  const double F = mh[RTX_M_F0] + mh[RTX_M_1MF0] * pow5(1.0 - VdotH);  // :291",
+         "  const double F = __builtin_fma(mh[RTX_M_1MF0], pow5(1.0 - VdotH), mh[RTX_M_F0]);  // :291"),
+        ("  const double denom = (NdotH * NdotH) * mh[RTX_M_A2M1] + 1.0;  // :295",
+         "  const double denom = __builtin_fma(NdotH * NdotH, mh[RTX_M_A2M1], 1.0);  // :295"),
+        ("  const double Dd = RTX_PI * ((denom * denom) + 1e-8);  // :296",
+         "  const double Dd = RTX_PI * __builtin_fma(denom, denom, 1e-8);  // :296"),
+        ("  const double dL = (NdotL + sqrt_shade(a2 + oma2 * (NdotL * NdotL))) + 1e-8;  // :299-301",
+         "  const double dL = (NdotL + sqrt_shade(__builtin_fma(oma2, NdotL * NdotL, a2))) + 1e-8;  // :299-301"),
+        ("  const double dV = (NdotV + sqrt_shade(a2 + oma2 * (NdotV * NdotV))) + 1e-8;",
+         "  const double dV = (NdotV + sqrt_shade(__builtin_fma(oma2, NdotV * NdotV, a2))) + 1e-8;"),
+        ("div_shade(1.0, Dd * ((4.0 * NdotV) + 1e-8));  // :306",
+         "div_shade(1.0, Dd * __builtin_fma(4.0, NdotV, 1e-8));  // :306"),
+        ("  const double sf = spec_base + g * glint;  // :315",
+         "  const double sf = __builtin_fma(g, glint, spec_base);  // :315"),
+        ("  const double ar = (0.004 + ((tr * dli) * litf) * dg) + sc[RTX_H_DOMEC + 0] * di;",
+         "  const double ar = __builtin_fma(sc[RTX_H_DOMEC + 0], di, __builtin_fma((tr * dli) * litf, dg, 0.004));"),
+        ("  const double ag = (0.004 + ((tg * dli) * litf) * dg) + sc[RTX_H_DOMEC + 1] * di;",
+         "  const double ag = __builtin_fma(sc[RTX_H_DOMEC + 1], di, __builtin_fma((tg * dli) * litf, dg, 0.004));"),
+        ("  const double ab = (0.004 + ((tb * dli) * litf) * dg) + sc[RTX_H_DOMEC + 2] * di;",
+         "  const double ab = __builtin_fma(sc[RTX_H_DOMEC + 2], di, __builtin_fma((tb * dli) * litf, dg, 0.004));"),
+        ("    const double r = (ip * hs) + (omhs * (1.0 - ip));  // :221",
+         "    const double r = __builtin_fma(ip, hs, omhs * (1.0 - ip));  // :221"),
+        ("    const double gg = (ip * omhs) + (hs * (1.0 - ip));  // :222",
+         "    const double gg = __builtin_fma(ip, omhs, hs * (1.0 - ip));  // :222"),
+        ("    const double b = 0.5 + 0.5 * ip;  // :223", "    const double b = __builtin_fma(0.5, ip, 0.5);  // :223"),
+        ("      cr = cr + thr * lr_;\n      cg = cg + thr * lg_;\n      cb = cb + thr * lb_;",
+         "      cr = __builtin_fma(thr, lr_, cr);\n      cg = __builtin_fma(thr, lg_, cg);\n      cb = __builtin_fma(thr, lb_, cb);"),
+    ]
+    for a, b in subs:
+        src = _sub(src, a, b)
+    return src
+
+
+PATCHES = {f.__name__: f for f in (shade_fma, abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
                                    lv_together, self_triple, lv_triple, tile_trace, persist_plain, block_plain)}
 
 
