@@ -25,9 +25,11 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"
                # MachineLICM hoists the ocml sin polynomial constants out of the bounce loop into VGPRs,
                # which then spill at 128 VGPRs; A/B (profiles/r1_ab_variants.txt): faster on every config
                "-mllvm", "-disable-machine-licm"]
-# rtx_small.hip only (the TREE = false kernels): the max-ilp machine scheduler (A/B in
-# profiles/r3_ab_variants.txt: C2 -0.5..-0.9%, C1 -2.4%; the culled kernels lose with it, C4 +1.4%)
-SMALL_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+# rtx_small.hip only (the TREE = false kernels). Round 3 built them with the max-ilp machine
+# scheduler (profiles/r3_ab_variants.txt: C2 -0.5..-0.9%, C1 -2.4%); with the forward fold of round 5
+# the default scheduler is the faster one (A/B r5i: C2 -0.8%, C1 -0.9%, C2main -0.4%). The unit
+# stays separate so that its flags can differ from the culled kernels'.
+SMALL_FLAGS: list = []
 
 
 def hipcc() -> str:

@@ -396,7 +396,70 @@ def shade_fma(src: str) -> str:
     return src
 
 
-PATCHES = {f.__name__: f for f in (shade_fma, abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
+def abl_noshadow_tree(src: str) -> str:
+    """Ablation (wrong output): culled scenes (TREE kernels) test no shadow ray (every hit lit)."""
+    return _sub(src, "  if (TREE && sc[RTX_H_SHGRID] != 0.0 && sc[RTX_H_TAME] != 0.0 &&",
+                "  if (TREE) {  // ablation\n  } else if (TREE && sc[RTX_H_SHGRID] != 0.0 && sc[RTX_H_TAME] != 0.0 &&")
+
+
+def var_nogrid(src: str) -> str:
+    """Variant (same output): no shadow-grid lookup; culled scenes' shadow rays walk the tree."""
+    return _sub(src, "  if (TREE && sc[RTX_H_SHGRID] != 0.0 && sc[RTX_H_TAME] != 0.0 &&",
+                "  if (false && TREE && sc[RTX_H_SHGRID] != 0.0 && sc[RTX_H_TAME] != 0.0 &&")
+
+
+def var_nobeam(src: str) -> str:
+    """Variant (same output): reflected rays walk the culling tree (no wave beam)."""
+    return _sub(src, "      if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(", "      if (false && BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(")
+
+
+def var_nofrustum(src: str) -> str:
+    """Variant (same output): camera rays walk the culling tree (no per-tile frustum candidates)."""
+    return _sub(src, "      fr = wave_frustum(p, __builtin_amdgcn_readfirstlane(col - lane % kWaveW),",
+                "      fr = false && wave_frustum(p, __builtin_amdgcn_readfirstlane(col - lane % kWaveW),")
+
+
+def abl_hoist_geo(src: str) -> str:
+    """Ablation (wrong output): the sphere loops of nearest_hit and of the small scenes' shadow test
+    read sphere 0's geometry every iteration (loop-invariant scalar loads, hoisted): what the scalar
+    loads' latency costs those loops."""
+    src = src.replace("    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;",
+                      "    const P* g0 = geo;  // ablation")
+    src = _sub(src, "      const G* g0 = geo + __builtin_amdgcn_readfirstlane(j + (j >= hs)) * RTX_GEOM_WORDS;\n"
+                    "      const G* g1 = geo + __builtin_amdgcn_readfirstlane(j + 1 + (j + 1 >= hs)) * RTX_GEOM_WORDS;",
+               "      const G* g0 = geo;  // ablation\n      const G* g1 = geo + RTX_GEOM_WORDS;")
+    return src
+
+
+def nobehind(src: str) -> str:
+    """Variant (same output): the 'sphere behind the origin' test leaves the skip flag; the root's
+    own sign test (valid: s1 > 0, implied false there) decides alone, two compares fewer per test."""
+    src = _sub(src, "    t.skip = !(t.d > 0.0) || (h > 0.0 && c >= 0.0);", "    t.skip = !(t.d > 0.0);")
+    return _sub(src, "    t.skip = !(t.d > 0.0) || behind(b, c);", "    t.skip = !(t.d > 0.0);")
+
+
+def spec_onercp(src: str) -> str:
+    """Variant (a few ulp): the specular's G and spec_base share one reciprocal."""
+    return _sub(src, """  const double G = ((2.0 * NdotL) * (2.0 * NdotV)) * div_shade(1.0, dL * dV);  // :303
+  const double spec_base = ((F * a2) * G) * div_shade(1.0, Dd * __builtin_fma(4.0, NdotV, 1e-8));  // :306""",
+                """  const double spec_base = ((F * a2) * ((2.0 * NdotL) * (2.0 * NdotV))) *
+                           div_shade(1.0, (dL * dV) * (Dd * __builtin_fma(4.0, NdotV, 1e-8)));  // :303-306""")
+
+
+def tk_early(src: str) -> str:
+    """Variant (same output): the hit's texture key (checker cell / texel) right after P, so that P
+    is dead across the shadow test and the specular (fewer live registers there)."""
+    old_tail = """  const double tex = mh[RTX_M_TEX];
+  s.tk = tex == RTX_TEX_CHECKER ? (trunc_parity(px * 2.0) == trunc_parity(pz * 2.0))  // :30
+         : tex != RTX_TEX_IMAGE ? 0
+         : IMG ? image_texel(mh, gh, px, py, pz) : -1;  // -1: an untextured k_render_fast build defers the ray
+"""
+    src = _sub(src, old_tail, "")
+    anchor = "  const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;  // :73\n"
+    return _sub(src, anchor, anchor + old_tail)
+
+
+PATCHES = {f.__name__: f for f in (tk_early, nobehind, spec_onercp, abl_hoist_geo, abl_noshadow_tree, var_nogrid, var_nobeam, var_nofrustum, shade_fma, abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
                                    lv_together, self_triple, lv_triple, tile_trace, persist_plain, block_plain)}
 
 
