@@ -99,9 +99,12 @@ enum {
                         mask k set unless sphere 64k+j provably cannot shadow (shader.py:126-128 in its
                         any-hit form) a shadow ray whose nudged origin lies in the voxel; last, the
                         huge spheres' mask (rays outside the grid that miss the ball) */
-  RTX_H_SINRED = 40  /* 1: every material's thin-film phase (shader.py:208, |phase| <= 10 pi |thickness|)
+  RTX_H_SINRED = 40, /* 1: every material's thin-film phase (shader.py:208, |phase| <= 10 pi |thickness|)
                         lies in the kernel sine's reduction range (|x| <= 2^20), so no lane needs a
                         range check; 0: checked per wave */
+  RTX_H_NBEAM = 41   /* culled scenes: spheres [NBEAM, S) are all huge (the culling tree's always-tested
+                        ones, RTX_H_NALWAYS): the level-0 tile candidates and the reflected-ray beams take
+                        them as candidates without a test; 0 = no such tail (older blobs) */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 #define RTX_SHGRID_WORDS 13 /* words of the shadow-grid record before its masks */

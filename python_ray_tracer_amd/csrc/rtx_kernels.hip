@@ -1306,6 +1306,12 @@ __device__ __forceinline__ void camera_ray(const Params& p, int col, int lr, dou
   oz = sc[RTX_H_CAM + 2];
 }
 
+// spheres [nb, nsph) are all huge (RTX_H_NBEAM): candidates of every tile and beam without a test
+__device__ __forceinline__ int huge_tail(const cdouble* sc, int nsph) {
+  const int nb = (int)sc[RTX_H_NBEAM];
+  return nb > 0 && nb < nsph ? nb : nsph;
+}
+
 // ---- level-0 candidates of a wave tile ------------------------------------------------------
 // The camera rays of a wave's pixels leave one origin O through points (x, y, 0) of the image
 // plane (camera_dir, base.py:123-141), and x (y) is monotone in the column (row), as is its
@@ -1354,8 +1360,10 @@ __device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, u
   const double oo = sc[RTX_H_CAMOO];
   const double* g = p.scene + RTX_HDR_WORDS;  // per-lane loads: a generic pointer
   const int lane = (int)__lane_id();
+  const int nb = huge_tail(sc, p.nsph);
   auto may = [&](int s) {
     if (s >= p.nsph) return false;
+    if (s >= nb) return true;  // a huge sphere of the scene's tail: a candidate without a test
     const double* e = g + s * RTX_GEOM_WORDS;
     const double wx = e[RTX_G_CX] - ox, wy = e[RTX_G_CY] - oy, wz = e[RTX_G_CZ] - oz;
     const double rr = e[RTX_G_RR];
@@ -1367,7 +1375,10 @@ __device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, u
     return !out;
   };
   m0 = __ballot(may(lane));
-  m1 = p.nsph > 64 ? __ballot(may(64 + lane)) : 0ull;
+  // the second pass only when a sphere above 63 needs its test (C4: 65 spheres, the 65th the ground)
+  m1 = p.nsph <= 64 ? 0ull
+       : nb > 64    ? __ballot(may(64 + lane))
+                    : (p.nsph >= 128 ? ~0ull : (uint64_t(1) << (p.nsph - 64)) - 1);
   return true;
 }
 
@@ -1432,6 +1443,7 @@ struct Beam {
   uint64_t ex;              // the active lanes
   int n;                    // their count
   int passes;
+  int nb;                   // spheres [nb, nsph): the huge tail, candidates without a test
 };
 __device__ __forceinline__ double rfl_d(double x) {
   const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(x));
@@ -1458,11 +1470,12 @@ __device__ __forceinline__ int pow2_above(double x, int lo, int hi) {
   return e < lo ? lo : e;
 }
 template <typename T>
-__device__ __forceinline__ bool wave_beam(const T* tab, int nsph, double ox, double oy, double oz, double dx,
+__device__ __forceinline__ bool wave_beam(const T* tab, int nb, double ox, double oy, double oz, double dx,
                                           double dy, double dz, Beam& bm) {
   bm.ex = __ballot(1);
   bm.n = __builtin_popcountll(bm.ex);
-  bm.passes = (nsph + bm.n - 1) / bm.n;
+  bm.nb = nb;
+  bm.passes = (nb + bm.n - 1) / bm.n;  // the huge tail [nb, nsph) is dealt out to nobody
   if (bm.passes > kBeamPasses) return false;
   const double Ox = rfl_d(ox), Oy = rfl_d(oy), Oz = rfl_d(oz);
   const double Ax = rfl_d(dx), Ay = rfl_d(dy), Az = rfl_d(dz);
@@ -1477,7 +1490,7 @@ __device__ __forceinline__ bool wave_beam(const T* tab, int nsph, double ox, dou
   const double om = __builtin_sqrt((Ox * Ox + Oy * Oy) + Oz * Oz) + rho;          // >= |O|
   const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm.ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm.ex, 0));
   auto may = [&](int s) {
-    if (s >= nsph) return false;
+    if (s >= nb) return false;
     const T* e = tab + s * RTX_GEOM_WORDS;
     const double wx = e[RTX_G_CX] - Ox, wy = e[RTX_G_CY] - Oy, wz = e[RTX_G_CZ] - Oz;
     const double rr = e[RTX_G_RR];
@@ -1502,7 +1515,7 @@ __device__ __forceinline__ bool wave_beam(const T* tab, int nsph, double ox, dou
 // Nearest hit over a wave beam's candidates (pass j, bit b: sphere j n + popcount(ex below b)),
 // pairs at a time like nearest_hit; in scene order.
 template <typename P, typename Wk>
-__device__ __forceinline__ void nearest_beam(const P* geo, const Beam& bm, double ox, double oy, double oz,
+__device__ __forceinline__ void nearest_beam(const P* geo, int nsph, const Beam& bm, double ox, double oy, double oz,
                                              double dx, double dy, double dz, double& tmin, int& hit, bool& tie,
                                              double tame, Wk& wk) {
   tmin = FARAWAY;
@@ -1533,6 +1546,22 @@ __device__ __forceinline__ void nearest_beam(const P* geo, const Beam& bm, doubl
         isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s0, tmin, hit, tie); });
       }
     }
+  }
+  // the huge tail, tested by every ray (wave-uniform bounds)
+  wk.test(nsph - bm.nb);
+  int s = bm.nb;
+  for (; s + 1 < nsph; s += 2) {
+    const P* g0 = geo + s * RTX_GEOM_WORDS;
+    const SphTest a0 = isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    const SphTest a1 = isect_disc(g0 + RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz, tame);
+    isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
+      nearest_update(v0, t0, s, tmin, hit, tie);
+      nearest_update(v1, t1, s + 1, tmin, hit, tie);
+    });
+  }
+  if (s < nsph) {
+    const SphTest a0 = isect_disc(geo + s * RTX_GEOM_WORDS, ox, oy, oz, oo, dx, dy, dz, tame);
+    isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s, tmin, hit, tie); });
   }
 }
 
@@ -1608,6 +1637,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const int nsph = p.nsph;
+  const int nb = TREE ? huge_tail(sc, nsph) : nsph;  // the beams' tested spheres
   // the half-b sphere test (SphTest): origins the kernel generates itself, in a tame scene
   const double tame = p.mode != 1 && p.mode != 3 && sc[RTX_H_TAME] != 0.0 ? 0x1.0p-350 : __builtin_nan("");
 
@@ -1858,13 +1888,13 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       // the wave's beam candidates (tame scenes up to 128 spheres), else the culling tree
       Beam bm;
       const double* btab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
-      if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(btab, nsph, ox, oy, oz, dx, dy, dz, bm)) {
+      if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(btab, nb, ox, oy, oz, dx, dy, dz, bm)) {
         if (st) stat_wave(st, RTX_S_BEAMW);
         for (int j = 0; j < bm.passes; ++j) {  // a lane's sphere test per pass, priced as two node tests
           wk.node();                            // (like wave_frustum)
           wk.node();
         }
-        nearest_beam(geo, bm, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+        nearest_beam(geo, nsph, bm, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else {
         nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       }

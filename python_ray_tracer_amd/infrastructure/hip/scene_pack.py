@@ -376,6 +376,11 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
     out = np.concatenate([blob, node_arr.ravel(), cgeo.ravel()])
     out[L.H_NNODES] = len(nodes)
     out[L.H_NALWAYS] = len(huge)
+    # RTX_H_NBEAM: the huge spheres that end the scene (typically the ground, appended last) are
+    # candidates of every tile frustum and reflected-ray beam without a test
+    out[L.H_NBEAM] = (max(small) + 1) if small else 0
+    if out[L.H_NBEAM] == S:
+        out[L.H_NBEAM] = 0
     out[L.H_NODES] = hdr_nodes
     out[L.H_CGEO] = hdr_cgeo
     return out

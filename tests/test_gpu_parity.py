@@ -17,6 +17,7 @@ import torch
 from oracle import numpy_oracle as O
 from python_ray_tracer_amd import scenes
 from tests.conftest import GOLDEN, golden_png
+from tests.specs import HUGE_LAYOUTS, huge_tail_spec
 
 pytestmark = pytest.mark.gpu
 
@@ -469,6 +470,22 @@ def test_big_scene_register_level_kernel(hip, B):
     want = O.render(O.scene_from_spec(spec), B, stats=st)
     assert np.abs(got - want).max() <= ATOL, np.abs(got - want).max()
     assert np.array_equal(O.to_uint8(got, 96, 54), O.to_uint8(want, 96, 54))
+    s = r.stats()
+    assert s["rays"] == st.rays and s["hits"] == st.hits
+
+
+@pytest.mark.parametrize("B", [3, 5])
+@pytest.mark.parametrize("layout", sorted(HUGE_LAYOUTS))
+def test_huge_tail_layouts(hip, layout, B):
+    """Huge spheres ending the scene (RTX_H_NBEAM: the tile frustums' and reflected-ray beams'
+    candidates without a test) before, at and after sphere 64, inside the scene, and absent; the
+    persistent culled kernel against the oracle: colour, uint8 and counters."""
+    spec = huge_tail_spec(layout, 80, 45)
+    r, got = _render(hip, spec, B, stats=True)
+    st = O.TraceStats()
+    want = O.render(O.scene_from_spec(spec), B, stats=st)
+    assert np.abs(got - want).max() <= ATOL, np.abs(got - want).max()
+    assert np.array_equal(O.to_uint8(got, 80, 45), O.to_uint8(want, 80, 45))
     s = r.stats()
     assert s["rays"] == st.rays and s["hits"] == st.hits
 

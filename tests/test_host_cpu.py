@@ -16,6 +16,7 @@ from python_ray_tracer_amd import scenes, tiling
 from python_ray_tracer_amd.infrastructure.hip import _lib as L
 from python_ray_tracer_amd.infrastructure.hip import scene_pack
 from tests.conftest import REPO
+from tests.specs import HUGE_LAYOUTS, huge_tail_spec
 
 
 def _header_functions():
@@ -69,6 +70,7 @@ def test_abi_layout_matches_header():
     assert const("RTX_H_TAME") == L.H_TAME
     assert const("RTX_H_SHGRID") == L.H_SHGRID
     assert const("RTX_H_SINRED") == L.H_SINRED
+    assert const("RTX_H_NBEAM") == L.H_NBEAM
     assert const("RTX_MAGIC") == L.MAGIC
     assert const("RTX_UNBOUNDED_LEVELS") == L.UNBOUNDED_LEVELS
     lay = (ctypes.c_int * 8)()
@@ -190,6 +192,7 @@ def test_culling_tree_invariants(n):
     nal = int(blob[L.H_NALWAYS])
     assert sorted(cg[:, L.G_IDX].astype(int).tolist()) == list(range(S))
     assert nal == 1 and int(cg[0, L.G_IDX]) == n  # the ground sphere (appended last) is always tested
+    assert int(blob[L.H_NBEAM]) == n  # ... and is the scene's huge tail (no frustum or beam test)
     for k in range(S):  # the culled list carries the same geometry words
         s = int(cg[k, L.G_IDX])
         assert np.array_equal(cg[k, :L.G_IDX], geo[s, :L.G_IDX])
@@ -667,3 +670,20 @@ def test_pack_sin_range_flag():
     assert scene_pack.pack_override(sc, sc.shapes[1], near)[L.H_SINRED] == 1.0
     sc.shapes[2].shader.thin_film_thickness = -1e5
     assert scene_pack.pack_scene(sc)[L.H_SINRED] == 0.0
+
+
+@pytest.mark.parametrize("layout", sorted(HUGE_LAYOUTS))
+def test_pack_huge_tail(layout):
+    """RTX_H_NBEAM: the first index of the huge spheres that end the scene (every later sphere huge,
+    so the kernel's tile frustums and reflected-ray beams take them without a test); 0 when the last
+    sphere is small."""
+    spec = huge_tail_spec(layout, 32, 18)
+    blob = scene_pack.pack_scene(scenes.build_scene(spec))
+    nb, S = int(blob[L.H_NBEAM]), len(spec["spheres"])
+    assert nb == HUGE_LAYOUTS[layout][-1]
+    radii = [sp["radius"] for sp in spec["spheres"]]
+    if nb:
+        assert all(r > scene_pack.HUGE_RADIUS for r in radii[nb:]) and radii[nb - 1] <= scene_pack.HUGE_RADIUS
+    else:
+        assert radii[-1] <= scene_pack.HUGE_RADIUS
+    assert 0 <= nb < S
