@@ -1719,9 +1719,9 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       tie = sc[RTX_H_MAT0] != 0.0;
     } else if (TREE && sc[RTX_H_NNODES] != 0.0) {
       if (fr) {
-        wk.node();  // the tile's plane tests, priced as two node tests per 64 spheres
+        wk.node();  // the tile's plane tests, priced as two node tests per 64 spheres tested
         wk.node();
-        if (nsph > 64) {
+        if (nb > 64) {
           wk.node();
           wk.node();
         }

@@ -404,7 +404,9 @@ def _append_culling_tree(blob: np.ndarray, geo: np.ndarray, S: int) -> np.ndarra
 # covers the small spheres and, for a light above them, their shadow on the plane of their lowest
 # point (where a ground under them is hit), at most 3x their extent.
 SHGRID_MAX_SPHERES = 128
-SHGRID_CELLS = 32  # cells along the grid's longest side (cubic cells)
+# cells along the grid's longest side (cubic cells): the first of these whose grid has at most
+# SHGRID_MAX_VOXELS voxels (48: C4 -1.8%, C5 -2%, C3 -0.4% against 32, A/B r5p; 64 no better)
+SHGRID_CELLS = (48, 32)
 SHGRID_MAX_VOXELS = 1 << 14
 
 
@@ -430,9 +432,12 @@ def _append_shadow_grid(blob: np.ndarray, geo: np.ndarray, S: int, lpos) -> np.n
         for ax in (0, 2):
             lo[ax] = max(min(lo[ax], proj[:, ax].min()), mid[ax] - 1.5 * (ext + 2 * pad))
             hi[ax] = min(max(hi[ax], proj[:, ax].max()), mid[ax] + 1.5 * (ext + 2 * pad))
-    cell = float((hi - lo).max()) / SHGRID_CELLS
-    dims = np.maximum(np.ceil((hi - lo) / cell), 1).astype(np.int64)
-    if int(np.prod(dims)) > SHGRID_MAX_VOXELS:
+    for cells in ((SHGRID_CELLS,) if np.isscalar(SHGRID_CELLS) else SHGRID_CELLS):
+        cell = float((hi - lo).max()) / cells
+        dims = np.maximum(np.ceil((hi - lo) / cell), 1).astype(np.int64)
+        if int(np.prod(dims)) <= SHGRID_MAX_VOXELS:
+            break
+    else:
         return blob
     inv = 1.0 / cell
     # voxel boxes (grown by a rounding margin: the kernel's index arithmetic may place q one voxel off

@@ -5,9 +5,12 @@
 Each variant renders the same packed scene with rtx_render_camera into its own output; per round
 and variant, `iters` launches are timed with HIP events (rtx_profile_* of that library). Prints the
 median and min per-launch kernel time, and checks every variant's output against the first.
+A variant `lib.so@NAME=VALUE+...` packs its own scene with those scene_pack constants set (host
+packer A/B: e.g. `ab/x.so@SHGRID_CELLS=48+SHGRID_MAX_VOXELS=65536`).
 """
 
 import argparse
+import ast
 import ctypes
 import statistics
 import sys
@@ -54,15 +57,33 @@ def main():
         from python_ray_tracer_amd.infrastructure.hip import scene_pack
 
         scene_pack.BVH_LEAF = a.bvh_leaf
+    from python_ray_tracer_amd.infrastructure.hip import scene_pack
+
     scene = scenes.build_scene(spec)
-    blob_np = pack_scene(scene)
     dev = torch.device("cuda", 0)
-    blob = torch.from_numpy(blob_np).to(dev)
-    S = int(blob_np[L.H_NSPH])
+
+    def pack(overrides):
+        saved = {k: getattr(scene_pack, k) for k in overrides}
+        try:
+            for k, v in overrides.items():
+                setattr(scene_pack, k, ast.literal_eval(v))
+            scene_pack._pack_static.cache_clear()
+            return pack_scene(scene)
+        finally:
+            for k, v in saved.items():
+                setattr(scene_pack, k, v)
+            scene_pack._pack_static.cache_clear()
+
+    paths, blobs = [], []
+    for arg in a.libs:
+        path, _, ov = arg.partition("@")
+        paths.append(path)
+        blobs.append(torch.from_numpy(pack(dict(kv.split("=") for kv in ov.split("+") if kv))).to(dev))
+    S = int(blobs[0][L.H_NSPH].item())
     W, H = spec["camera"]["width"], spec["camera"]["height"]
     n = W * H
     kind = {"f32": L.OUT_F32_SOA, "f64": L.OUT_F64_SOA, "u8": L.OUT_U8_HWC}[a.out]
-    libs = [open_lib(p) for p in a.libs]
+    libs = [open_lib(p) for p in paths]
     outs, wss = [], []
     for lib in libs:
         outs.append(torch.empty(3 * n * (8 if a.out == "f64" else 4 if a.out == "f32" else 1), dtype=torch.uint8,
@@ -71,7 +92,7 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def launch(k):
-        rc = libs[k].rtx_render_camera(blob.data_ptr(), S, W, H, 1, 1, 0, H, B, outs[k].data_ptr(), kind,
+        rc = libs[k].rtx_render_camera(blobs[k].data_ptr(), S, W, H, 1, 1, 0, H, B, outs[k].data_ptr(), kind,
                                        wss[k].data_ptr(), wss[k].numel(), None, stream)
         assert rc == 0, libs[k].rtx_last_error()
 
@@ -102,7 +123,7 @@ def main():
         same = torch.equal(outs[k], outs[0])
         t = times[k]
         km = statistics.median(t)
-        print(f"{Path(p).name:28s} median {km:9.2f} us  min {min(t):9.2f} us  "
+        print(f"{Path(p.partition('@')[0]).name + p.partition('@')[1] + p.partition('@')[2]:28s} median {km:9.2f} us  min {min(t):9.2f} us  "
               f"Mpix/s(kernel) {n / km if km else float('nan'):10.1f}  e2e/frame {statistics.median(e2e[k]):9.2f} us  "
               f"equal_to_first={same}")
 
