@@ -333,8 +333,8 @@ def main():
                                        "wave_searches": sum(st["waves_traced"][1:])},
                     "note": "15/primary ray + 20/ray-sphere test + 22/culling-node test + 200/shaded hit over the "
                             "tests k_render_fast executed (kernel counters); node_tests prices the culling tree's "
-                            "box tests (box_tests) and, as node tests too, the level-0 frustum planes, shadow-grid "
-                            "lookups and beam passes; `achieved` above prices every test the reference performs "
+                            "box tests (box_tests) and, as node tests too, the shadow-grid lookups and beam passes (the "
+                            "level-0 tile candidates' image-plane box comparisons are not priced); `achieved` above prices every test the reference performs "
                             "(S per ray), culled or not"},
                 "lane_utilisation": {
                     "traced": [round(r / (64 * w), 4) if w else None for r, w in zip(st["rays"], st["waves_traced"])],

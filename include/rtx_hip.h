@@ -102,9 +102,13 @@ enum {
   RTX_H_SINRED = 40, /* 1: every material's thin-film phase (shader.py:208, |phase| <= 10 pi |thickness|)
                         lies in the kernel sine's reduction range (|x| <= 2^20), so no lane needs a
                         range check; 0: checked per wave */
-  RTX_H_NBEAM = 41   /* culled scenes: spheres [NBEAM, S) are all huge (the culling tree's always-tested
+  RTX_H_NBEAM = 41,  /* culled scenes: spheres [NBEAM, S) are all huge (the culling tree's always-tested
                         ones, RTX_H_NALWAYS): the level-0 tile candidates and the reflected-ray beams take
                         them as candidates without a test; 0 = no such tail (older blobs) */
+  RTX_H_SBOX = 42    /* culled scenes of at most 128 spheres: word offset of S records {x lo, x hi, y lo,
+                        y hi}, each sphere's image-plane box for this camera: a camera ray through (x, y, 0)
+                        outside it provably yields FARAWAY for that sphere (bounds may be infinite);
+                        0 = none (the level-0 tile candidates then take the frustum-plane test) */
 };
 #define RTX_MAGIC 5527384.0 /* 'RTX1' */
 #define RTX_SHGRID_WORDS 13 /* words of the shadow-grid record before its masks */

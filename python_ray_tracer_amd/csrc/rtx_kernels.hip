@@ -1314,18 +1314,21 @@ __device__ __forceinline__ int huge_tail(const cdouble* sc, int nsph) {
 
 // ---- level-0 candidates of a wave tile ------------------------------------------------------
 // The camera rays of a wave's pixels leave one origin O through points (x, y, 0) of the image
-// plane (camera_dir, base.py:123-141), and x (y) is monotone in the column (row), as is its
-// rounding, so every lane's vector v = (fl(x - Ox), fl(y - Oy), VZ) lies in the rectangle spanned
-// by the four corner vectors of the tile's extreme columns and rows. The rays therefore lie in the
-// pyramid bounded by the four planes through O and two adjacent corners. A sphere whose ball,
-// expanded by the culling margin lm (node_may_hit: a root the reference reports lies within lm of
-// the ball), is wholly outside one of those planes yields FARAWAY for every ray of the tile, so
-// the tile's level-0 nearest hit may skip it: with scale = |C - O|^2 + 2|C|^2 + 3r^2 + |O|^2
-// (>= node_may_hit's scale for a single sphere), lm = 1e-7 (scale + 1), doubled here like the
-// node margin (it also absorbs the rounding of the corner cross products and dot products,
-// ~1e-15 relative, and |D| = 1 +- 1e-15). Comparisons are written so that NaN keeps the sphere.
-// One lane tests one sphere (two passes for 65..128 spheres); the ballots are the tile's candidate
-// masks. Needs the full wave (call before any lane diverges).
+// plane (camera_dir, base.py:123-141), and x (y) is monotone in the column (row), so the plane
+// points of the tile's lanes lie in the rectangle of its extreme columns and rows (a lane's ray
+// passes through O + (fl(x - Ox), fl(y - Oy), VZ), within an ulp of (x, y, 0)). The host gives every
+// sphere an image-plane box for this camera (RTX_H_SBOX, scene_pack.sphere_plane_boxes): a camera
+// ray through a plane point outside it yields FARAWAY for that sphere. The box is built from the
+// sphere's radius expanded by the culling margin lm (node_may_hit: a root the reference reports lies
+// within lm of the ball), with scale = |C - O|^2 + 2|C|^2 + 3r^2 + |O|^2 (>= node_may_hit's scale for
+// a single sphere) and lm = 1e-7 (scale + 1), doubled like the node margin: that also absorbs
+// |D| = 1 +- 1e-15 and the plane point's ulp. A sphere whose box misses the tile's rectangle is
+// skipped by the tile's level-0 nearest hit: the nearest hit and the tie flag are unchanged.
+// Comparisons are written so that NaN keeps the sphere; the huge tail (RTX_H_NBEAM) is kept without
+// a test. One lane tests one sphere (two passes for 65..128 spheres); the ballots are the tile's
+// candidate masks. Needs the full wave (call before any lane diverges). (Rounds 3-4 tested each
+// sphere against the tile's four frustum planes, ~40 VALU a lane; A/B r5q: the boxes take C3 -7.6%,
+// C4 -4.9%, C5 -3.8%.)
 __device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, uint64_t& m0, uint64_t& m1) {
   const cdouble* sc = (const cdouble*)p.scene;
   const int W = p.width;
@@ -1340,39 +1343,16 @@ __device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, u
     return (sc[RTX_H_YFIX] != 0.0 && r == H - 1) ? sc[RTX_H_YSTOP] : (double)r * sc[RTX_H_YSTEP] + sc[RTX_H_YSTART];
   };
   const double xa = xv(c0), xb = xv(c1), ya = yv(global_row(p, lr0)), yb = yv(global_row(p, l1));
-  const double ox = sc[RTX_H_CAM + 0], oy = sc[RTX_H_CAM + 1], oz = sc[RTX_H_CAM + 2];
-  const double x0 = __builtin_fmin(xa, xb) - ox, x1 = __builtin_fmax(xa, xb) - ox;
-  const double y0 = __builtin_fmin(ya, yb) - oy, y1 = __builtin_fmax(ya, yb) - oy;
-  const double v = sc[RTX_H_VZ];
-  // corners A (x0, y0), B (x1, y0), C (x1, y1), D (x0, y1), counter-clockwise in the image plane;
-  // n = sign(VZ) (a x b) points into the pyramid for each edge (a, b)
-  const double sg = v > 0.0 ? 1.0 : -1.0;
-  const double ax[4] = {x0, x1, x1, x0}, ay[4] = {y0, y0, y1, y1};
-  double nx[4], ny[4], nz[4], nl[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int j = (k + 1) & 3;
-    nx[k] = sg * ((ay[k] * v) - (v * ay[j]));
-    ny[k] = sg * ((v * ax[j]) - (ax[k] * v));
-    nz[k] = sg * ((ax[k] * ay[j]) - (ay[k] * ax[j]));
-    nl[k] = __builtin_sqrt((nx[k] * nx[k] + ny[k] * ny[k]) + nz[k] * nz[k]);
-  }
-  const double oo = sc[RTX_H_CAMOO];
-  const double* g = p.scene + RTX_HDR_WORDS;  // per-lane loads: a generic pointer
+  const double xlo = __builtin_fmin(xa, xb), xhi = __builtin_fmax(xa, xb);
+  const double ylo = __builtin_fmin(ya, yb), yhi = __builtin_fmax(ya, yb);
+  const double* bx = p.scene + (int64_t)sc[RTX_H_SBOX];  // per-lane loads: a generic pointer
   const int lane = (int)__lane_id();
   const int nb = huge_tail(sc, p.nsph);
   auto may = [&](int s) {
     if (s >= p.nsph) return false;
-    if (s >= nb) return true;  // a huge sphere of the scene's tail: a candidate without a test
-    const double* e = g + s * RTX_GEOM_WORDS;
-    const double wx = e[RTX_G_CX] - ox, wy = e[RTX_G_CY] - oy, wz = e[RTX_G_CZ] - oz;
-    const double rr = e[RTX_G_RR];
-    const double scale = (((wx * wx + wy * wy) + wz * wz) + 2.0 * e[RTX_G_CC]) + 3.0 * rr + oo;
-    const double m = __builtin_sqrt(rr) + 2e-7 * (scale + 1.0);
-    bool out = false;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out = out || ((nx[k] * wx + ny[k] * wy) + nz[k] * wz < -(m * nl[k]));
-    return !out;
+    if (s >= nb) return true;
+    const double* e = bx + 4 * s;
+    return !(e[1] < xlo || e[0] > xhi || e[3] < ylo || e[2] > yhi);
   };
   m0 = __ballot(may(lane));
   // the second pass only when a sphere above 63 needs its test (C4: 65 spheres, the 65th the ground)
@@ -1689,7 +1669,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   uint64_t fm0 = 0, fm1 = 0;
   bool fr = false;
   if constexpr (TREE) {
-    if (cam0 && nsph <= 128 && sc[RTX_H_NNODES] != 0.0 && sc[RTX_H_TAME] != 0.0 && sc[RTX_H_VZ] != 0.0) {
+    if (cam0 && nsph <= 128 && sc[RTX_H_NNODES] != 0.0 && sc[RTX_H_SBOX] != 0.0 && sc[RTX_H_TAME] != 0.0 &&
+        sc[RTX_H_VZ] != 0.0) {
       const int lane = threadIdx.x & 63;
       fr = wave_frustum(p, __builtin_amdgcn_readfirstlane(col - lane % kWaveW),
                         __builtin_amdgcn_readfirstlane(lr - lane / kWaveW), fm0, fm1);
@@ -1718,13 +1699,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       // with that material, deferred like a tie
       tie = sc[RTX_H_MAT0] != 0.0;
     } else if (TREE && sc[RTX_H_NNODES] != 0.0) {
-      if (fr) {
-        wk.node();  // the tile's plane tests, priced as two node tests per 64 spheres tested
-        wk.node();
-        if (nb > 64) {
-          wk.node();
-          wk.node();
-        }
+      if (fr) {  // (the image-plane boxes' comparisons are not priced)
         nearest_masked<true>(geo, fm0, fm1, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else if (cam0) {
         nearest_bvh<true>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);

@@ -51,7 +51,8 @@ H_MAGIC, H_NSPH, H_CAM, H_LIGHT, H_DOMEC, H_NDOME, H_DOMEI = 0, 1, 2, 5, 8, 11, 
 H_XSTART, H_XSTEP, H_XSTOP, H_XFIX = 20, 21, 22, 23
 H_YSTART, H_YSTEP, H_YSTOP, H_YFIX = 24, 25, 26, 27
 H_VZ, H_VZ2, H_W, H_H, H_CAMOO = 28, 29, 30, 31, 32
-H_NNODES, H_NALWAYS, H_NODES, H_CGEO, H_TAME, H_MAT0, H_SHGRID, H_SINRED, H_NBEAM = 33, 34, 35, 36, 37, 38, 39, 40, 41
+H_NNODES, H_NALWAYS, H_NODES, H_CGEO, H_TAME, H_MAT0, H_SHGRID, H_SINRED, H_NBEAM, H_SBOX = (
+    33, 34, 35, 36, 37, 38, 39, 40, 41, 42)
 SIN_TFT_MAX = 2.0 ** 20 / (10.0 * 3.141592653589793 * 1.001)  # thin-film thickness bound of RTX_H_SINRED
 SHGRID_WORDS = 13
 TAME_BOUND = 2.0 ** 60

@@ -165,6 +165,10 @@ def _pack_static(static: tuple) -> np.ndarray:
         blob = _append_culling_tree(blob, geo.copy(), S)
         if S <= SHGRID_MAX_SPHERES:  # (the kernel reads the grid only with a culling tree)
             blob = _append_shadow_grid(blob, geo.copy(), S, lpos)
+        if S <= SBOX_MAX_SPHERES:  # image-plane boxes, unbounded until _apply_camera fills them
+            off = blob.size
+            blob = np.concatenate([blob, np.tile([-np.inf, np.inf, -np.inf, np.inf], S)])
+            blob[L.H_SBOX] = off
     # image textures: one float64 RGB texel table per distinct image, after everything else; the
     # material's RTX_M_TR word holds its word offset
     textures, offsets, size = [], {}, blob.size
@@ -269,6 +273,59 @@ def _apply_camera(blob: np.ndarray, cpos, W: int, H: int) -> None:
         co = (geo[:, L.G_CX] * ox + geo[:, L.G_CY] * oy) + geo[:, L.G_CZ] * oz
         geo[:, L.G_C0] = ((geo[:, L.G_CC] + cw["oo"]) - 2 * co) - geo[:, L.G_RR]
     h[L.H_TAME] = 1.0 if is_tame(tables[0].reshape(S, L.GEOM_WORDS), cpos) else 0.0
+    if h[L.H_SBOX]:
+        off = int(h[L.H_SBOX])
+        blob[off: off + 4 * S] = sphere_plane_boxes(tables[0].reshape(S, L.GEOM_WORDS), cpos).ravel()
+
+
+# --- image-plane boxes (RTX_H_SBOX) -----------------------------------------------------------
+# A camera ray leaves O through the image-plane point (x, y, 0) (base.py:123-141: direction
+# norm(x - Ox, y - Oy, 0 - Oz)). Projected on the xz plane, a ray that comes within R of the centre
+# C passes within R of (Cx, Cz) (projection shortens distances), so its plane point's x lies where
+# the half-lines from (Ox, Oz) through (x, 0) meet the disc (Cx, Cz; R): between the two tangents'
+# crossings of z = 0, both tangent directions heading towards the plane (else unbounded); likewise
+# y on the yz plane. R is r plus the doubled culling margin (rtx_kernels.hip wave_frustum), which
+# covers the reference root's rounding and the ray direction's normalisation; the box is padded for this function's own rounding and for
+# the lane's plane point Ox + fl(x - Ox), within an ulp of x.
+SBOX_MAX_SPHERES = 128
+SBOX_MIN_TZ = 1e-3  # tangent directions closer than this to the image plane: an unbounded side
+
+
+def sphere_plane_boxes(geo: np.ndarray, cpos) -> np.ndarray:
+    """[S, 4] {x lo, x hi, y lo, y hi}: camera rays through image-plane points outside a sphere's box
+    yield FARAWAY for it (NumpySphere.intersect, shape.py:28-51); infinite bounds where none hold."""
+    O = np.asarray(cpos, dtype=np.float64)
+    C = geo[:, L.G_CX:L.G_CZ + 1]
+    rr = geo[:, L.G_RR]
+    w = C - O
+    scale = ((w * w).sum(axis=1) + 2.0 * geo[:, L.G_CC]) + 3.0 * rr + float(O @ O)
+    R = (np.sqrt(rr) + 2e-7 * (scale + 1.0)) * (1.0 + 1e-9)
+    vz = 0.0 - O[2]
+    out = np.tile(np.array([-np.inf, np.inf, -np.inf, np.inf]), (len(geo), 1))
+    if not (vz != 0.0 and np.all(np.isfinite(O))):
+        return out
+    sg = 1.0 if vz > 0 else -1.0
+    with np.errstate(all="ignore"):
+        for k, a in enumerate((0, 1)):
+            wa, wz = w[:, a], w[:, 2]
+            d = np.sqrt(wa * wa + wz * wz)
+            ua, uz = wa / d, wz / d
+            sa = R / d
+            ca = np.sqrt(np.maximum(1.0 - sa * sa, 0.0))
+            xs, ok = [], (d > R * (1.0 + 1e-9)) & np.isfinite(d) & np.isfinite(R)
+            for sgn in (1.0, -1.0):  # the two tangent directions: u rotated by +-alpha
+                ta = ua * ca - sgn * uz * sa
+                tz = uz * ca + sgn * ua * sa
+                ok &= sg * tz > SBOX_MIN_TZ
+                x = O[a] + vz * (ta / tz)
+                pad = 1e-9 * (np.abs(x) + abs(O[a]) + 1.0) + 1e-12 * abs(vz) / (tz * tz)
+                xs.append((x - pad, x + pad))
+            lo = np.minimum(xs[0][0], xs[1][0])
+            hi = np.maximum(xs[0][1], xs[1][1])
+            ok &= np.isfinite(lo) & np.isfinite(hi)
+            out[ok, 2 * k] = lo[ok]
+            out[ok, 2 * k + 1] = hi[ok]
+    return out
 
 
 def is_tame(geo: np.ndarray, cpos) -> bool:

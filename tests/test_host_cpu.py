@@ -71,6 +71,7 @@ def test_abi_layout_matches_header():
     assert const("RTX_H_SHGRID") == L.H_SHGRID
     assert const("RTX_H_SINRED") == L.H_SINRED
     assert const("RTX_H_NBEAM") == L.H_NBEAM
+    assert const("RTX_H_SBOX") == L.H_SBOX
     assert const("RTX_MAGIC") == L.MAGIC
     assert const("RTX_UNBOUNDED_LEVELS") == L.UNBOUNDED_LEVELS
     lay = (ctypes.c_int * 8)()
@@ -687,3 +688,53 @@ def test_pack_huge_tail(layout):
     else:
         assert radii[-1] <= scene_pack.HUGE_RADIUS
     assert 0 <= nb < S
+
+
+@pytest.mark.parametrize("case", ["c4", "c3", "cam_ahead", "cam_behind", "inside", "near_plane"])
+def test_plane_boxes_are_conservative(case):
+    """RTX_H_SBOX (scene_pack.sphere_plane_boxes): every camera ray the reference's intersect
+    (shape.py:28-51) reports a hit for passes through an image-plane point inside that sphere's box,
+    for every pixel of a small frame and for dense plane points around each bounded box; shrinking
+    the boxes by 0.5% of their size loses hits (the test has teeth)."""
+    spec = scenes.random_spec(64 if case == "c4" else 16, 3, 160, 90)
+    cam = {"c4": None, "c3": None, "cam_ahead": [0.4, 0.8, -0.7], "cam_behind": [0.3, 0.9, 18.0],
+           "inside": None, "near_plane": [0.0, 0.6, -0.05]}[case]
+    if cam is not None:
+        spec["camera"]["position"] = cam
+    if case == "inside":  # the camera inside a sphere: that sphere's box is unbounded
+        spec["spheres"][0]["center"] = [float(v) + 0.1 for v in spec["camera"]["position"]]
+        spec["spheres"][0]["radius"] = 0.8
+    sc = O.scene_from_spec(spec)
+    blob = scene_pack.pack_scene(scenes.build_scene(spec))
+    off = int(blob[L.H_SBOX])
+    assert off > 0
+    S = len(sc.spheres)
+    box = blob[off:off + 4 * S].reshape(S, 4)
+    ox, oy, oz = sc.cam
+    W, H = sc.width, sc.height
+    aspect = W / H
+    px = np.tile(np.linspace(-1, 1, W), H)
+    py = np.repeat(np.linspace(1 / aspect + 0.25, -1 / aspect + 0.25, H), W)
+    rng = np.random.default_rng(5)
+    for b in box:  # dense points around each bounded box
+        if np.all(np.isfinite(b)):
+            cx, cy, ex, ey = (b[0] + b[1]) / 2, (b[2] + b[3]) / 2, (b[1] - b[0]) * 0.6, (b[3] - b[2]) * 0.6
+            px = np.concatenate([px, rng.uniform(cx - ex, cx + ex, 3000)])
+            py = np.concatenate([py, rng.uniform(cy - ey, cy + ey, 3000)])
+    dx, dy, dz = O._norm(px - ox, py - oy, 0 - oz)
+    hits = lost = 0
+    for j, sp in enumerate(sc.spheres):
+        hit = O.intersect(sp, ox, oy, oz, dx, dy, dz) < O.FARAWAY
+        lo_x, hi_x, lo_y, hi_y = box[j]
+        inside = (px >= lo_x) & (px <= hi_x) & (py >= lo_y) & (py <= hi_y)
+        assert not (hit & ~inside).any(), (case, j, box[j], int((hit & ~inside).sum()))
+        hits += int(hit.sum())
+        if np.all(np.isfinite(box[j])):
+            sx, sy = (hi_x - lo_x) * 0.005, (hi_y - lo_y) * 0.005
+            shrunk = (px >= lo_x + sx) & (px <= hi_x - sx) & (py >= lo_y + sy) & (py <= hi_y - sy)
+            lost += int((hit & ~shrunk).sum())
+    assert hits > 100, hits
+    if case != "inside":
+        assert lost > 0, case
+    if case == "inside":
+        assert np.all(np.isinf(box[0]))
