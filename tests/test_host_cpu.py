@@ -149,7 +149,7 @@ def test_pack_matches_reference_expressions():
     S = len(spec["spheres"])
     assert blob[L.H_NSPH] == S and blob[L.H_MAGIC] == L.MAGIC
     geo = blob[L.HDR_WORDS:L.HDR_WORDS + S * L.GEOM_WORDS].reshape(S, -1)
-    mat = blob[L.HDR_WORDS + S * L.GEOM_WORDS:].reshape(S, -1)
+    mat = blob[L.HDR_WORDS + S * L.GEOM_WORDS:L.HDR_WORDS + S * (L.GEOM_WORDS + L.MAT_WORDS)].reshape(S, -1)
     # level-0 "c" of shape.py:35-37 equals the oracle's scalar evaluation
     for s, sp in enumerate(spec["spheres"]):
         cx, cy, cz = sp["center"]
