@@ -142,6 +142,10 @@ template <bool DEEP = false, bool TREE = true>
 __host__ __device__ constexpr size_t level_lds_bytes(int B) {
   return (size_t)level_lds_slots<DEEP>(B) * fast_block<TREE>() * (4 * 8 + 4);
 }
+// The one-tile culled kernels (TP 1, capped: the forward fold) accumulate the pixel colour in LDS
+// after the scene table ([3][block] doubles, each lane its own slots) instead of three VGPR pairs:
+// at 96 VGPRs (5 waves/SIMD) one of them spilled to scratch on every level (C3 traffic 1.5x).
+constexpr size_t kColourLdsBytes = 3 * sizeof(double) * 256;
 // the general kernel's nearest pass walks the culling tree from this many spheres on (A/B: 65
 // spheres -11%, 17 spheres +2..6%: its depth-first lanes diverge, so a wave-uniform walk pays less)
 constexpr int kGeneralTreeMin = 32;
@@ -1568,6 +1572,14 @@ __device__ __forceinline__ unsigned char quant_u8(double c) {
   return v >= 0.0 ? (unsigned char)(int)v : (unsigned char)0;
 }
 
+// The lane's index in its wave by two VALU instructions the compiler cannot merge with an earlier
+// lane id, so that a value derived from it is recomputed instead of kept live (fast_tile's tail).
+__device__ __forceinline__ int lane_id_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 __device__ __forceinline__ void write_out(const Params& p, int64_t i, double r, double g, double b) {
   // the frame is written once and never read back by the kernel: streaming (nontemporal) stores
   // (A/B, identical output: C5 -1.5..-1.9%, C3 -0.9%, C2 -0.4..-0.8%)
@@ -1626,15 +1638,28 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   int kb = 0;                  // absolute level of this launch's first ray (mode 2: the resumed level)
   const double* rin = nullptr;  // mode 2: the chain's resume record (levels 0..kb-1)
   int col = 0, lr = 0;         // mode 0: the pixel's column and local row
+  // WX x WY waves per block; wave w -> WW x WH sub-tile, lane -> (l % WW, l / WW)
+  // (wave_tile: (bx, by) is this wave's own WW x WH tile; TREE only, so WW = kWaveW there)
+  constexpr int WW = wave_w<TREE>(), WH = 64 / WW, WX = waves_x<TREE>(), WY = fast_waves<TREE>() / WX;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // the wave in the block
+  // The pixel index (modes 0, 1, 3) from the block's tile, the wave and a lane id. The culled
+  // kernels' write-out recomputes it from a fresh lane id (lane_id_fresh): kept live across the
+  // bounce loop, the 64-bit index spilled in the one-tile culled kernels (C3) and cost the persistent
+  // one registers (A/B r5v: C4 -1.8%); the small-scene kernels keep it (C2 +1.4% recomputed).
+  auto pixel_index = [&](int lane) -> int64_t {
+    if (p.mode == 0) {
+      const int c = wave_tile ? bx * WW + (lane % WW) : bx * (WX * WW) + (wv % WX) * WW + (lane % WW);
+      const int r = wave_tile ? by * WH + (lane / WW) : by * (WY * WH) + (wv / WX) * WH + (lane / WW);
+      return (int64_t)r * p.width + c;
+    }
+    return (int64_t)bx * FB + wv * 64 + lane;
+  };
   if (p.mode == 0) {
-    // WX x WY waves per block; wave w -> WW x WH sub-tile, lane -> (l % WW, l / WW)
-    // (wave_tile: (bx, by) is this wave's own WW x WH tile; TREE only, so WW = kWaveW there)
-    constexpr int WW = wave_w<TREE>(), WH = 64 / WW, WX = waves_x<TREE>(), WY = fast_waves<TREE>() / WX;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = TREE ? wv : (int)(threadIdx.x >> 6);
     col = wave_tile ? bx * WW + (lane % WW) : bx * (WX * WW) + (w % WX) * WW + (lane % WW);
     lr = wave_tile ? by * WH + (lane / WW) : by * (WY * WH) + (w / WX) * WH + (lane / WW);
     active = col < p.width && lr < p.n_rows;
-    i = (int64_t)lr * p.width + col;
+    if constexpr (!TREE) i = (int64_t)lr * p.width + col;  // (kept live: A/B r5v C2 +1.4% recomputed)
   } else if (!DEEP || p.mode == 1 || p.mode == 3) {
     i = (int64_t)bx * FB + threadIdx.x;
     active = i < p.n;
@@ -1716,6 +1741,14 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     if (first) __syncthreads();
   }
   if (!active) return;
+  constexpr bool CL = kForwardFold && !DEEP && LDS && TREE && !BEAM;  // colour in LDS (kColourLdsBytes)
+  static_assert(!CL || 3 * sizeof(double) * FB == kColourLdsBytes, "colour LDS");
+  double* const cl = CL ? const_cast<double*>(lds_tab) + nsph * kSphWords + threadIdx.x : nullptr;
+  if constexpr (CL) {
+    cl[0] = 0.0;
+    cl[FB] = 0.0;
+    cl[2 * FB] = 0.0;
+  }
 
   // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level), or,
   // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
@@ -1772,7 +1805,8 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       deferred = true;
       appended = true;
       rays_through = hits_through = kb + B;
-      const int64_t slot = append_deferred(p, deferred_entry(i, p.frame, kb + B, kb + B));
+      const int64_t slot =
+          append_deferred(p, deferred_entry(p.mode == 2 || !TREE ? i : pixel_index(lane_id_fresh()), p.frame, kb + B, kb + B));
       if (p.drec && slot >= 0 && slot < p.rec_cap && kb + B == p.drec_level) {
         double* rec = p.drec + slot * rec_words(kb + B);
         double rx = dx, ry = dy, rz = dz;
@@ -1807,9 +1841,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       double lr_, lg_, lb_;
       hit_color<IMG>(tab + nsph * RTX_GEOM_WORDS + hit * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted, s.spec,
                      s.va, 0.0, 0.0, 0.0, lr_, lg_, lb_);
-      cr = __builtin_fma(thr, lr_, cr);
-      cg = __builtin_fma(thr, lg_, cg);
-      cb = __builtin_fma(thr, lb_, cb);
+      if constexpr (CL) {
+        cl[0] = __builtin_fma(thr, lr_, cl[0]);
+        cl[FB] = __builtin_fma(thr, lg_, cl[FB]);
+        cl[2 * FB] = __builtin_fma(thr, lb_, cl[2 * FB]);
+      } else {
+        cr = __builtin_fma(thr, lr_, cr);
+        cg = __builtin_fma(thr, lg_, cg);
+        cb = __builtin_fma(thr, lb_, cb);
+      }
       if (!weighted || k >= B) break;
       thr = (thr * 0.5) * s.g;  // the reflection's weight, (R * 0.5) * g (shader.py:106)
     } else if (!weighted || k >= B || at_cap) {
@@ -1893,9 +1933,15 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_add(st, RTX_S_BOXES, wk.boxes);
     }
   }
+  const int64_t io = (DEEP && p.mode == 2) || !TREE ? i : pixel_index(lane_id_fresh());
+  if constexpr (CL) {
+    cr = cl[0];
+    cg = cl[FB];
+    cb = cl[2 * FB];
+  }
   if (deferred) {
     // a tie (deep deferrals were appended with their resume record)
-    if (!appended) append_deferred(p, deferred_entry(i, p.frame, rays_through, hits_through));
+    if (!appended) append_deferred(p, deferred_entry(io, p.frame, rays_through, hits_through));
     if (st && !rin) stat_add(st, RTX_S_DEFERRED, 1);
     return;
   }
@@ -1941,7 +1987,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
                 cr, cg, cb, cr, cg, cb);
     }
   }
-  write_out(p, i, cr, cg, cb);
+  write_out(p, io, cr, cg, cb);
 }
 
 // TP: 0 = no culling tree and no persistent launch (scenes below kTreeMinSpheres), 1 = culling tree,
@@ -2550,7 +2596,8 @@ template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   const bool small = p.nsph < kTreeMinSpheres;  // the TREE = false kernels: fast_block<false>() threads
   const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
-                     (LVL ? (small ? level_lds_bytes<DEEP, false>(B) : level_lds_bytes<DEEP>(B)) : 0);
+                     (LVL ? (small ? level_lds_bytes<DEEP, false>(B) : level_lds_bytes<DEEP>(B)) : 0) +
+                     (kForwardFold && !DEEP && !small && p.n_fetch == 0 ? kColourLdsBytes : 0);  // TP 1
   if (p.n_fetch == 0) {  // one tile per block: the instantiations without the persistent loop
     if (p.nsph < kTreeMinSpheres) {  // TP 0: the rtx_small.hip unit
       const hipError_t e =

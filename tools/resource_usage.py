@@ -25,8 +25,8 @@ FLAGS = [f for f in _build.HIPCC_FLAGS if f not in ("-fPIC", "-shared")]
 
 
 def demangle_args(name: str) -> str:
-    m = re.search(r"k_render_fastILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELi(\d)E", name)
-    return "<{},{},{},{},{},{}>".format(*m.groups()) if m else name
+    m = re.search(r"k_render_fastILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)E", name)
+    return "<{},{},{},{},{},{},{}>".format(*m.groups()) if m else name
 
 
 def usage(text: str) -> dict:
