@@ -165,10 +165,10 @@ def _pack_static(static: tuple) -> np.ndarray:
         blob = _append_culling_tree(blob, geo.copy(), S)
         if S <= SHGRID_MAX_SPHERES:  # (the kernel reads the grid only with a culling tree)
             blob = _append_shadow_grid(blob, geo.copy(), S, lpos)
-        if S <= SBOX_MAX_SPHERES:  # image-plane boxes, unbounded until _apply_camera fills them
-            off = blob.size
-            blob = np.concatenate([blob, np.tile([-np.inf, np.inf, -np.inf, np.inf], S)])
-            blob[L.H_SBOX] = off
+    if SBOX_MIN_SPHERES <= S <= SBOX_MAX_SPHERES:  # image-plane boxes, unbounded until _apply_camera fills them
+        off = blob.size
+        blob = np.concatenate([blob, np.tile([-np.inf, np.inf, -np.inf, np.inf], S)])
+        blob[L.H_SBOX] = off
     # image textures: one float64 RGB texel table per distinct image, after everything else; the
     # material's RTX_M_TR word holds its word offset
     textures, offsets, size = [], {}, blob.size
@@ -287,6 +287,10 @@ def _apply_camera(blob: np.ndarray, cpos, W: int, H: int) -> None:
 # y on the yz plane. R is r plus the doubled culling margin (rtx_kernels.hip wave_frustum), which
 # covers the reference root's rounding and the ray direction's normalisation; the box is padded for this function's own rounding and for
 # the lane's plane point Ox + fl(x - Ox), within an ulp of x.
+# the culled kernels (from BVH_MIN_SPHERES): the small-scene kernels gain nothing from them (A/B r5t,
+# r5y-r5zd: C2 +10% with the level-0 tests skipped, however the candidates are built; tools/ab_patches.py
+# small_boxes*, packed with SBOX_MIN_SPHERES=1)
+SBOX_MIN_SPHERES = 8
 SBOX_MAX_SPHERES = 128
 SBOX_MIN_TZ = 1e-3  # tangent directions closer than this to the image plane: an unbounded side
 

@@ -22,6 +22,7 @@ Where each experiment's result lives:
 | ``v_always`` | variant | V normalised for every hit: within noise (r3f) |
 | ``lv_together`` / ``self_triple`` / ``lv_triple`` | variant | ILP in shade(): r3p, not adopted |
 | ``tile_trace`` | instrument | per-tile start/end timestamps of k_render_fast (``tools/tile_trace.py``) |
+| ``small_boxes`` .. ``small_boxes8`` | variant / instrument | image-plane box candidates for the small-scene kernels' level-0 rays, five ways (pack with ``@SBOX_MIN_SPHERES=1``): all C2 +10..12%; the mask computed and left unused costs the same, a never-taken pair-skip branch alone +0.7% (r5t, r5y-r5zc) |
 
 (The round-2/3 patches were written against the source of their session; their anchors are kept
 as they were, so they document the experiment and re-apply to that revision with ``--rev``.)
@@ -459,7 +460,230 @@ def tk_early(src: str) -> str:
     return _sub(src, anchor, anchor + old_tail)
 
 
-PATCHES = {f.__name__: f for f in (tk_early, nobehind, spec_onercp, abl_hoist_geo, abl_noshadow_tree, var_nogrid, var_nobeam, var_nofrustum, shade_fma, abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
+def small_boxes(src: str) -> str:
+    """Variant (same output): the image-plane box candidates (RTX_H_SBOX) also for the small-scene
+    kernels' level-0 rays (pack with SBOX_MIN_SPHERES=1)."""
+    src = _sub(src, """__device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, uint64_t& m0, uint64_t& m1) {
+  const cdouble* sc = (const cdouble*)p.scene;
+  const int W = p.width;
+  if (c0 >= W || lr0 >= p.n_rows) return false;  // no pixel of this wave lies in the frame
+  const int c1 = c0 + kWaveW - 1 < W - 1 ? c0 + kWaveW - 1 : W - 1;
+  const int l1 = lr0 + kWaveH - 1 < p.n_rows - 1 ? lr0 + kWaveH - 1 : p.n_rows - 1;""",
+               """template <int TW = kWaveW, int TH = kWaveH>
+__device__ __forceinline__ bool wave_frustum(const Params& p, int c0, int lr0, uint64_t& m0, uint64_t& m1) {
+  const cdouble* sc = (const cdouble*)p.scene;
+  const int W = p.width;
+  if (c0 >= W || lr0 >= p.n_rows) return false;  // no pixel of this wave lies in the frame
+  const int c1 = c0 + TW - 1 < W - 1 ? c0 + TW - 1 : W - 1;
+  const int l1 = lr0 + TH - 1 < p.n_rows - 1 ? lr0 + TH - 1 : p.n_rows - 1;""")
+    src = _sub(src, """  if constexpr (TREE) {
+    if (cam0 && nsph <= 128 && sc[RTX_H_NNODES] != 0.0 && sc[RTX_H_SBOX] != 0.0 && sc[RTX_H_TAME] != 0.0 &&
+        sc[RTX_H_VZ] != 0.0) {
+      const int lane = threadIdx.x & 63;
+      fr = wave_frustum(p, __builtin_amdgcn_readfirstlane(col - lane % kWaveW),
+                        __builtin_amdgcn_readfirstlane(lr - lane / kWaveW), fm0, fm1);
+    }
+  }""", """  if constexpr (TREE) {
+    if (cam0 && nsph <= 128 && sc[RTX_H_NNODES] != 0.0 && sc[RTX_H_SBOX] != 0.0 && sc[RTX_H_TAME] != 0.0 &&
+        sc[RTX_H_VZ] != 0.0) {
+      const int lane = threadIdx.x & 63;
+      fr = wave_frustum(p, __builtin_amdgcn_readfirstlane(col - lane % kWaveW),
+                        __builtin_amdgcn_readfirstlane(lr - lane / kWaveW), fm0, fm1);
+    }
+  } else {
+    if (cam0 && sc[RTX_H_SBOX] != 0.0 && sc[RTX_H_TAME] != 0.0 && sc[RTX_H_VZ] != 0.0) {
+      constexpr int TW = wave_w<false>();
+      const int lane = threadIdx.x & 63;
+      fr = wave_frustum<TW, 64 / TW>(p, __builtin_amdgcn_readfirstlane(col - lane % TW),
+                                     __builtin_amdgcn_readfirstlane(lr - lane / TW), fm0, fm1);
+    }
+  }""")
+    src = _sub(src, """    } else if (cam0) {
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else {
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    }
+  }
+  if constexpr (LDS) {""", """    } else if (fr) {
+      nearest_masked<true>(geo, fm0, 0ull, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else if (cam0) {
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else {
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    }
+  }
+  if constexpr (LDS) {""")
+    return src
+
+
+def small_boxes2(src: str) -> str:
+    """Variant (same output): small_boxes with the tile's candidate mask built by a wave-uniform loop
+    over the spheres' boxes through the scalar cache (no per-lane global load at the wave's start)."""
+    src = small_boxes(src)
+    src = _sub(src, """      fr = wave_frustum<TW, 64 / TW>(p, __builtin_amdgcn_readfirstlane(col - lane % TW),
+                                     __builtin_amdgcn_readfirstlane(lr - lane / TW), fm0, fm1);""",
+               """      const int c0 = __builtin_amdgcn_readfirstlane(col - lane % TW);
+      const int lr0 = __builtin_amdgcn_readfirstlane(lr - lane / TW);
+      const int W = p.width, H = p.height;
+      if (c0 < W && lr0 < p.n_rows) {
+        const int c1 = c0 + TW - 1 < W - 1 ? c0 + TW - 1 : W - 1;
+        const int l1 = lr0 + 64 / TW - 1 < p.n_rows - 1 ? lr0 + 64 / TW - 1 : p.n_rows - 1;
+        auto xv = [&](int c) {
+          return (sc[RTX_H_XFIX] != 0.0 && c == W - 1) ? sc[RTX_H_XSTOP] : (double)c * sc[RTX_H_XSTEP] + sc[RTX_H_XSTART];
+        };
+        auto yv = [&](int r) {
+          return (sc[RTX_H_YFIX] != 0.0 && r == H - 1) ? sc[RTX_H_YSTOP] : (double)r * sc[RTX_H_YSTEP] + sc[RTX_H_YSTART];
+        };
+        const double xa = xv(c0), xb = xv(c1), ya = yv(global_row(p, lr0)), yb = yv(global_row(p, l1));
+        const double xlo = __builtin_fmin(xa, xb), xhi = __builtin_fmax(xa, xb);
+        const double ylo = __builtin_fmin(ya, yb), yhi = __builtin_fmax(ya, yb);
+        const cdouble* bxs = sc + (int)sc[RTX_H_SBOX];
+        uint64_t m = 0;
+        for (int s = 0; s < nsph; ++s) {
+          const cdouble* e = bxs + 4 * s;
+          if (!(e[1] < xlo || e[0] > xhi || e[3] < ylo || e[2] > yhi)) m |= uint64_t(1) << s;
+        }
+        fm0 = m;
+        fr = true;
+      }""")
+    return src
+
+
+def small_boxes3(src: str) -> str:
+    """Variant (same output): small_boxes2's mask, but the level-0 loop keeps nearest_hit's pair
+    structure and skips a pair (wave-uniform branch) when neither sphere is a candidate."""
+    src = small_boxes2(src)
+    src = _sub(src, """    } else if (fr) {
+      nearest_masked<true>(geo, fm0, 0ull, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else if (cam0) {""", """    } else if (cam0) {""")
+    src = _sub(src, """    } else if (cam0) {
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else {
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    }
+  }
+  if constexpr (LDS) {""", """    } else if (cam0) {
+      nearest_hit<true>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk, fr ? fm0 : ~0ull);
+    } else {
+      nearest_hit<false>(geo, nsph, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    }
+  }
+  if constexpr (LDS) {""")
+    src = _sub(src, """                                            double dy, double dz, double& tmin, int& hit, bool& tie, double tame,
+                                            Wk& wk) {
+  wk.test(nsph);""", """                                            double dy, double dz, double& tmin, int& hit, bool& tie, double tame,
+                                            Wk& wk, uint64_t cand = ~0ull) {
+  wk.test(nsph);""")
+    src = _sub(src, """  for (; s + 1 < nsph; s += 2) {
+    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const P* g1 = g0 + RTX_GEOM_WORDS;
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)""", """  for (; s + 1 < nsph; s += 2) {
+    if (((cand >> s) & 3ull) == 0) continue;  // neither sphere of the pair can be hit (wave-uniform)
+    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const P* g1 = g0 + RTX_GEOM_WORDS;
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)""")
+    src = _sub(src, """  if (s < nsph) {
+    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s, tmin, hit, tie); });
+  }
+}""", """  if (s < nsph && ((cand >> s) & 1ull)) {
+    const P* g0 = geo + __builtin_amdgcn_readfirstlane(s) * RTX_GEOM_WORDS;
+    const SphTest a0 = CAM ? isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame)
+                           : isect_disc(g0, ox, oy, oz, oo, dx, dy, dz, tame);
+    isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s, tmin, hit, tie); });
+  }
+}""")
+    return src
+
+
+def small_boxes4(src: str) -> str:
+    """Instrument: small_boxes3 with the mask computed but every pair tested (what the mask costs)."""
+    src = small_boxes3(src)
+    return _sub(src, "tmin, hit, tie, tame, wk, fr ? fm0 : ~0ull);", "tmin, hit, tie, tame, wk, fr ? (fm0 | ~0ull) : ~0ull);")
+
+
+def small_boxes5(src: str) -> str:
+    """Instrument: small_boxes3 without the mask (fr never set), only the pair-skip branch compiled."""
+    src = small_boxes3(src)
+    return _sub(src, """        fm0 = m;
+        fr = true;""", """        fm0 = m;
+        fr = m == 0x123456789ull;""")
+
+
+def small_boxes6(src: str) -> str:
+    """Variant (same output): small_boxes2's mask turned into a packed list of the candidates' indices
+    (4 bits each, scene order); the level-0 loop keeps nearest_hit's pair shape over that list."""
+    src = small_boxes2(src)
+    src = _sub(src, """    } else if (fr) {
+      nearest_masked<true>(geo, fm0, 0ull, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else if (cam0) {""", """    } else if (fr) {
+      nearest_list(geo, fm0, (int)fm1, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
+    } else if (cam0) {""")
+    src = _sub(src, """        fm0 = m;
+        fr = true;""", """        uint64_t lst = 0;
+        int k = 0;
+        for (int s = 0; s < nsph; ++s) {
+          if ((m >> s) & 1ull) {
+            lst |= (uint64_t)s << (4 * k);
+            ++k;
+          }
+        }
+        fm0 = lst;
+        fm1 = (uint64_t)k;
+        fr = true;""")
+    src = _sub(src, """// (x)^5 and (x)^2.5 for x in [0, 1]""", """// level-0 nearest hit over a packed candidate list (4-bit sphere indices in scene order, k of them)
+template <typename P, typename Wk>
+__device__ __forceinline__ void nearest_list(const P* geo, uint64_t lst, int k, double ox, double oy, double oz,
+                                             double dx, double dy, double dz, double& tmin, int& hit, bool& tie,
+                                             double tame, Wk& wk) {
+  wk.test(k);
+  tmin = FARAWAY;
+  hit = -1;
+  tie = false;
+  int j = 0;
+  for (; j + 1 < k; j += 2) {
+    const int s0 = __builtin_amdgcn_readfirstlane((int)((lst >> (4 * j)) & 15));
+    const int s1 = __builtin_amdgcn_readfirstlane((int)((lst >> (4 * j + 4)) & 15));
+    const P* g0 = geo + s0 * RTX_GEOM_WORDS;
+    const P* g1 = geo + s1 * RTX_GEOM_WORDS;
+    const SphTest a0 = isect_disc_cam(g0, ox, oy, oz, dx, dy, dz, tame);
+    const SphTest a1 = isect_disc_cam(g1, ox, oy, oz, dx, dy, dz, tame);
+    isect_pair(a0, a1, [&](double t0, bool v0, double t1, bool v1) {
+      nearest_update(v0, t0, s0, tmin, hit, tie);
+      nearest_update(v1, t1, s1, tmin, hit, tie);
+    });
+  }
+  if (j < k) {
+    const int s0 = __builtin_amdgcn_readfirstlane((int)((lst >> (4 * j)) & 15));
+    const SphTest a0 = isect_disc_cam(geo + s0 * RTX_GEOM_WORDS, ox, oy, oz, dx, dy, dz, tame);
+    isect_one(a0, [&](double t0, bool v0) { nearest_update(v0, t0, s0, tmin, hit, tie); });
+  }
+}
+
+// (x)^5 and (x)^2.5 for x in [0, 1]""")
+    return src
+
+
+def small_boxes7(src: str) -> str:
+    """Instrument: only nearest_hit's pair-skip branch, with a candidate mask of all ones the
+    compiler cannot see (no box mask computed)."""
+    src = small_boxes3(src)
+    src = _sub(src, "tmin, hit, tie, tame, wk, fr ? fm0 : ~0ull);",
+               "tmin, hit, tie, tame, wk, ~(uint64_t)(p.width == -5));")
+    return src
+
+
+def small_boxes8(src: str) -> str:
+    """Instrument: the box mask computed (kept live through an opaque test) and nothing skipped."""
+    src = small_boxes3(src)
+    src = _sub(src, "tmin, hit, tie, tame, wk, fr ? fm0 : ~0ull);",
+               "tmin, hit, tie, tame, wk, ~0ull);\n      if (fr && fm0 == 0x123456789ull) tmin = 0.0;")
+    return src
+
+
+PATCHES = {f.__name__: f for f in (small_boxes8, small_boxes7, small_boxes6, small_boxes5, small_boxes4, small_boxes3, small_boxes2, small_boxes, tk_early, nobehind, spec_onercp, abl_hoist_geo, abl_noshadow_tree, var_nogrid, var_nobeam, var_nofrustum, shade_fma, abl_noshadow_small, abl_nospec, abl_noirid, nu_select, inlgen, nogen, tinygen, nolit, noshadow, pair_nobranch, tex_select, v_always,
                                    lv_together, self_triple, lv_triple, tile_trace, persist_plain, block_plain)}
 
 
