@@ -1453,6 +1453,15 @@ __device__ __forceinline__ int pow2_above(double x, int lo, int hi) {
   const int e = __builtin_amdgcn_frexp_exp(x);  // x = m 2^e, m in [0.5, 1)
   return e < lo ? lo : e;
 }
+// sqrt for the beam's culling test: the hardware reciprocal square root and two Newton steps
+// (relative error far below 1e-13; the callers scale by 1 -+ 1e-13 towards keeping the sphere).
+// 0 and inf give NaN, which the test's comparisons read as "keep the sphere".
+__device__ __forceinline__ double sqrt_cull(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
+  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
+  return x * y;
+}
 template <typename T>
 __device__ __forceinline__ bool wave_beam(const T* tab, int nb, double ox, double oy, double oz, double dx,
                                           double dy, double dz, Beam& bm) {
@@ -1478,13 +1487,14 @@ __device__ __forceinline__ bool wave_beam(const T* tab, int nb, double ox, doubl
     const T* e = tab + s * RTX_GEOM_WORDS;
     const double wx = e[RTX_G_CX] - Ox, wy = e[RTX_G_CY] - Oy, wz = e[RTX_G_CZ] - Oz;
     const double rr = e[RTX_G_RR];
-    const double w = __builtin_sqrt((wx * wx + wy * wy) + wz * wz);
-    const double wr = w + rho;
+    const double wq = sqrt_cull((wx * wx + wy * wy) + wz * wz);
+    const double w = wq * (1.0 - 1e-13);         // <= |W|
+    const double wr = wq * (1.0 + 1e-13) + rho;  // >= |W| + rho
     const double lm = 4e-7 * ((((wr * wr + 2.0 * e[RTX_G_CC]) + 3.0 * rr) + om * om) + 1.0);
-    const double R = ((__builtin_sqrt(rr) + lm) + rho) * (1.0 + 1e-12);
+    const double R = ((sqrt_cull(rr) * (1.0 + 1e-13) + lm) + rho) * (1.0 + 1e-12);
     if (!(w > R)) return true;
     const double aw = (Ax * wx + Ay * wy) + Az * wz;
-    const double rhs = ct * __builtin_sqrt((w - R) * (w + R)) - st * R;
+    const double rhs = ct * (sqrt_cull((w - R) * (w + R)) * (1.0 - 1e-13)) - st * R;
     return !(aw < rhs - 1e-9 * ((w + R) + 1.0));
   };
   int cand = 0;

@@ -587,12 +587,13 @@ def _beam_candidates(G, Oc, A, r2, omc, drop_rho=False):
     ct, st = 1 - 2.0 ** ea, np.sqrt(2.0 ** (ea + 1)) * (1 + 1e-12)
     om = np.sqrt(Oc @ Oc) + rho
     Wv = G[:, :3] - Oc
-    w = np.sqrt((Wv ** 2).sum(1))
+    wq = np.sqrt((Wv ** 2).sum(1))
+    w = wq * (1 - 1e-13)  # the kernel's bounds around its approximate square roots (sqrt_cull)
     rr, CC = G[:, 3] ** 2, (G[:, :3] ** 2).sum(1)
-    lm = 4e-7 * ((((w + rho) ** 2 + 2 * CC) + 3 * rr) + om * om + 1)
-    R = (np.sqrt(rr) + lm + rho) * (1 + 1e-12)
+    lm = 4e-7 * ((((wq * (1 + 1e-13) + rho) ** 2 + 2 * CC) + 3 * rr) + om * om + 1)
+    R = (np.sqrt(rr) * (1 + 1e-13) + lm + rho) * (1 + 1e-12)
     with np.errstate(invalid="ignore"):
-        rhs = ct * np.sqrt((w - R) * (w + R)) - st * R
+        rhs = ct * (np.sqrt((w - R) * (w + R)) * (1 - 1e-13)) - st * R
     return ~(w > R) | ~(Wv @ A < rhs - 1e-9 * ((w + R) + 1))
 
 
