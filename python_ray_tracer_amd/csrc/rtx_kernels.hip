@@ -228,7 +228,11 @@ constexpr int kLevelMask = 0x7F;  // 7-bit level fields (level + 1)
 // (origin, direction) and the colour inputs (dli, di, spec, va, key) of levels 0..L; the general
 // kernel continues the chain at level L + 1 instead of re-rendering it from level 0.
 constexpr int kRecLevelWords = 5;
-__host__ __device__ constexpr int rec_words(int level) { return 6 + kRecLevelWords * (level + 1); }
+// With the forward fold (kForwardFold) the DEEP kernels' record is the next ray, the colour
+// accumulated through level L and the throughput of level L + 1: 10 words whatever L.
+__host__ __device__ constexpr int rec_words(int level) {
+  return kForwardFold ? 10 : 6 + kRecLevelWords * (level + 1);
+}
 constexpr int kDeepLevel2 = 2 * kDeepLevels + 1;  // deferral level of the first continuation pass
 constexpr int kDeepLevel3 = 3 * kDeepLevels + 2;  // ... and of the second
 static_assert(kDeepLevel3 + 2 < kLevelMask, "deferred-entry level fields hold 7 bits");
@@ -1762,7 +1766,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 
   // shift register of the non-terminal levels' colour inputs (slot 0 = most recent level), or,
   // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
-  constexpr bool LV = LVL && LDS && B > 0;
+  constexpr bool LV = LVL && LDS && B > 0 && !kForwardFold;
   constexpr int NS = B > 0 ? B : 1;
   constexpr int NL = LV ? level_lds_slots<DEEP>(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
   constexpr int NR = LV ? (B > NL ? B - NL : 1) : NS;
@@ -1774,8 +1778,16 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   int depth = 0;
   double cr = 0.0, cg = 0.0, cb = 0.0;
   // kForwardFold (capped kernels): colour accumulated level by level, thr = T_k
-  constexpr bool FWD = kForwardFold && !DEEP;
+  constexpr bool FWD = kForwardFold;
   double thr = 1.0;
+  if constexpr (FWD && DEEP) {  // a continued chain: its colour so far and the next level's weight
+    if (rin) {
+      cr = rin[6];
+      cg = rin[7];
+      cb = rin[8];
+      thr = rin[9];
+    }
+  }
   bool deferred = false, appended = false;
   int rays_through = 0, hits_through = -1;  // per-level counts already made for this pixel
 
@@ -1810,7 +1822,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     const bool weighted = s.lit && s.g != 0.0;
     // the cap itself (absolute level; a continuation pass may run into a cap of 9 or 10)
     const bool at_cap = DEEP && p.max_bounces >= 0 && kb + k >= p.max_bounces;
-    if (DEEP && weighted && k >= B && !at_cap) {  // the chain goes on beyond this kernel's levels
+    if (!FWD && DEEP && weighted && k >= B && !at_cap) {  // the chain goes on beyond this kernel's levels
       // k == B: levels kb..kb+B-1 are in the shift register (slot j = level kb+B-1-j), kb+B in s
       deferred = true;
       appended = true;
@@ -1860,7 +1872,24 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         cg = __builtin_fma(thr, lg_, cg);
         cb = __builtin_fma(thr, lb_, cb);
       }
-      if (!weighted || k >= B) break;
+      if (DEEP && weighted && k >= B && !at_cap) {  // the chain goes on beyond this kernel's levels
+        deferred = true;
+        appended = true;
+        rays_through = hits_through = kb + B;
+        const int64_t slot = append_deferred(p, deferred_entry(p.mode == 2 || !TREE ? i : pixel_index(lane_id_fresh()),
+                                                               p.frame, kb + B, kb + B));
+        if (p.drec && slot >= 0 && slot < p.rec_cap && kb + B == p.drec_level) {
+          double* rec = p.drec + slot * rec_words(kb + B);
+          double rx = dx, ry = dy, rz = dz;
+          reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
+          rec[0] = s.qx; rec[1] = s.qy; rec[2] = s.qz;
+          rec[3] = rx; rec[4] = ry; rec[5] = rz;
+          rec[6] = cr; rec[7] = cg; rec[8] = cb;
+          rec[9] = (thr * 0.5) * s.g;  // the next level's weight, as below
+        }
+        break;
+      }
+      if (!weighted || k >= B || at_cap) break;
       thr = (thr * 0.5) * s.g;  // the reflection's weight, (R * 0.5) * g (shader.py:106)
     } else if (!weighted || k >= B || at_cap) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
@@ -1989,7 +2018,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       }
     }
   }
-  if constexpr (DEEP) {  // a continued chain: fold on through the levels of its record (same fold)
+  if constexpr (DEEP && !FWD) {  // a continued chain: fold on through the levels of its record (same fold)
     for (int l = kb - 1; l >= 0; --l) {
       const double* lv = rin + 6 + kRecLevelWords * l;
       const int key = (int)lv[4];
@@ -2113,10 +2142,9 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
 // ------------------------------------------------------------------------------------------
 
 // frame fields: the ray, its nearest distance, the next shape to examine (-1: new ray), the
-// running colour sum over its hits (base.py:100-119), and the pending hit whose reflection is
-// being traced (its colour inputs).
-enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_TMIN, F_NEXT, F_AR, F_AG, F_AB,
-       F_DLI, F_DI, F_SPEC, F_VA, F_KEY, F_LEFT };  // F_LEFT: hits of this ray not yet shaded
+// weight of its hits (the product of (0.5 g) along the path to it), the hit whose reflection is
+// being traced, and the hits of the ray not yet shaded.
+enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_TMIN, F_NEXT, F_THR, F_KEY, F_LEFT };
 static_assert(F_LEFT < kFrameWords, "frame layout");
 
 struct Stack {
@@ -2126,16 +2154,19 @@ struct Stack {
   __device__ __forceinline__ double& at(int d, int f) const { return base[((int64_t)d * kFrameWords + f) * nw + w]; }
 };
 
-// rays_through / hits_through: per-level counts the fast kernel already made for this pixel
-// rec: a resume record (deep deferral) or null. With a record, frames 0..L hold the levels the fast
-// kernel shaded, each with its single hit pending (its colour inputs, nothing accumulated yet), and
-// the walk starts with the level L + 1 ray; their fold below is the fast kernel's fold, instruction
-// for instruction (hit_color with lit and weighted set).
+// rays_through / hits_through: per-level counts the fast kernel already made for this pixel.
+// The walk sums every shaded hit's colour with a black reflection, weighted by the product of
+// (0.5 g) along its path (shader.py:106-110 unrolled: the sum over the tree of hits, ties included,
+// base.py:100-119), in depth-first order: on a chain without ties these are the fast kernels'
+// forward-fold operations in their order, so a pixel's colour does not depend on which kernel
+// traced which of its levels. rec: a resume record (deep deferral: the next ray, the colour summed
+// through level L and level L + 1's weight), the walk starting at depth L + 1; or null.
 template <typename Stk>
 __device__ void trace_general(const Params& p, const Stk& S, double ox0, double oy0, double oz0, double dx0,
                               double dy0, double dz0, double& cr, double& cg, double& cb, int rays_through,
                               int hits_through, const double* rec = nullptr, int h_given = -1,
                               double t_given = 0.0) {
+  static_assert(kForwardFold, "the general kernel sums forwards, like the fast kernels");
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
   const double* tab = p.scene + RTX_HDR_WORDS;
@@ -2147,23 +2178,21 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
   unsigned long long* st = p.stats;
 
   int d = 0;
+  double ar = 0.0, ag = 0.0, ab = 0.0, thr0 = 1.0;
   if (rec) {
-    const int L = rays_through;
-    for (int l = 0; l <= L; ++l) {
-      const double* lv = rec + 6 + kRecLevelWords * l;
-      S.at(l, F_DLI) = lv[0]; S.at(l, F_DI) = lv[1]; S.at(l, F_SPEC) = lv[2]; S.at(l, F_VA) = lv[3];
-      S.at(l, F_KEY) = lv[4];
-      S.at(l, F_AR) = 0.0; S.at(l, F_AG) = 0.0; S.at(l, F_AB) = 0.0;
-      S.at(l, F_NEXT) = (double)(key_hit((int)lv[4]) + 1);
-      S.at(l, F_LEFT) = 1.0;
-    }
-    d = L + 1;
+    d = rays_through + 1;
+    ar = rec[6];
+    ag = rec[7];
+    ab = rec[8];
+    thr0 = rec[9];
     ox0 = rec[0]; oy0 = rec[1]; oz0 = rec[2];
     dx0 = rec[3]; dy0 = rec[4]; dz0 = rec[5];
   }
+  const int d0 = d;  // the depth whose finished ray ends the walk
   S.at(d, F_OX) = ox0; S.at(d, F_OY) = oy0; S.at(d, F_OZ) = oz0;
   S.at(d, F_DX) = dx0; S.at(d, F_DY) = dy0; S.at(d, F_DZ) = dz0;
   S.at(d, F_NEXT) = -1.0;
+  S.at(d, F_THR) = thr0;
   for (;;) {
     const double ox = S.at(d, F_OX), oy = S.at(d, F_OY), oz = S.at(d, F_OZ);
     const double dx = S.at(d, F_DX), dy = S.at(d, F_DY), dz = S.at(d, F_DZ);
@@ -2198,7 +2227,6 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       left = (tmin != FARAWAY || (d == 0 && h_given >= 0)) ? nh : 0;  // (nearest != FARAWAY) & (t == nearest), base.py:102-103
       S.at(d, F_TMIN) = tmin;
       S.at(d, F_LEFT) = (double)left;
-      S.at(d, F_AR) = 0.0; S.at(d, F_AG) = 0.0; S.at(d, F_AB) = 0.0;  // NumpyRGBColor(0, 0, 0)
       if (left > 0) h = first;
     } else {
       tmin = S.at(d, F_TMIN);
@@ -2212,22 +2240,13 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
         }
       }
     }
-    if (h == nsph) {  // this ray is done: its colour is the accumulated sum
-      const double rr = S.at(d, F_AR), rg = S.at(d, F_AG), rb = S.at(d, F_AB);
-      if (d == 0) {
-        cr = rr; cg = rg; cb = rb;
+    if (h == nsph) {  // this ray is done (its hits' colours are in the sum)
+      if (d == d0) {
+        cr = ar; cg = ag; cb = ab;
         return;
       }
-      --d;  // fold into the parent's pending hit (shader.py:106-110), then add (base.py:119)
-      const int key = (int)S.at(d, F_KEY);
-      const int ph = key_hit(key);
-      double xr, xg, xb;
-      hit_color<true>((d == 0 && mat0) ? mat0 : mtab + ph * RTX_MAT_WORDS, sc, S.at(d, F_DLI), S.at(d, F_DI),
-                      key_tex(key), true, true, S.at(d, F_SPEC), S.at(d, F_VA), rr, rg, rb, xr, xg, xb);
-      S.at(d, F_AR) = S.at(d, F_AR) + xr;
-      S.at(d, F_AG) = S.at(d, F_AG) + xg;
-      S.at(d, F_AB) = S.at(d, F_AB) + xb;
-      S.at(d, F_NEXT) = (double)(ph + 1);
+      --d;  // back to the parent ray: on to its next hit
+      S.at(d, F_NEXT) = (double)(key_hit((int)S.at(d, F_KEY)) + 1);
       S.at(d, F_LEFT) = S.at(d, F_LEFT) - 1.0;
       continue;
     }
@@ -2242,18 +2261,19 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
       atomicOr((uint32_t*)p.ws + RTX_WS_STATUS, (uint32_t)RTX_ST_STACK_OVERFLOW);
       descend = false;
     }
+    // this hit's colour with a black reflection, weighted (the fast kernels' forward fold)
+    const double thr = S.at(d, F_THR);
+    double xr, xg, xb;
+    hit_color<true>((d == 0 && mat0) ? mat0 : mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted,
+                    s.spec, s.va, 0.0, 0.0, 0.0, xr, xg, xb);
+    ar = __builtin_fma(thr, xr, ar);
+    ag = __builtin_fma(thr, xg, ag);
+    ab = __builtin_fma(thr, xb, ab);
     if (!descend) {
-      double xr, xg, xb;
-      hit_color<true>((d == 0 && mat0) ? mat0 : mtab + h * RTX_MAT_WORDS, sc, s.dli, s.di, s.tk, s.lit, weighted,
-                      s.spec, s.va, 0.0, 0.0, 0.0, xr, xg, xb);
-      S.at(d, F_AR) = S.at(d, F_AR) + xr;
-      S.at(d, F_AG) = S.at(d, F_AG) + xg;
-      S.at(d, F_AB) = S.at(d, F_AB) + xb;
       S.at(d, F_NEXT) = (double)(h + 1);
       S.at(d, F_LEFT) = (double)(left - 1);
       continue;
     }
-    S.at(d, F_DLI) = s.dli; S.at(d, F_DI) = s.di; S.at(d, F_SPEC) = s.spec; S.at(d, F_VA) = s.va;
     S.at(d, F_KEY) = (double)level_key(h, s.tk);
     double rx = dx, ry = dy, rz = dz;
     reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
@@ -2261,6 +2281,7 @@ __device__ void trace_general(const Params& p, const Stk& S, double ox0, double 
     S.at(d, F_OX) = s.qx; S.at(d, F_OY) = s.qy; S.at(d, F_OZ) = s.qz;
     S.at(d, F_DX) = rx; S.at(d, F_DY) = ry; S.at(d, F_DZ) = rz;
     S.at(d, F_NEXT) = -1.0;
+    S.at(d, F_THR) = (thr * 0.5) * s.g;  // the reflection's weight, (R * 0.5) * g (shader.py:106)
   }
 }
 
