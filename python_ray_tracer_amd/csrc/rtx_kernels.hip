@@ -2660,7 +2660,8 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
   Params p = p0;
   if (p.nsph <= kLdsMaxSpheres) {
     if constexpr (DEEP) {
-      if (kLevelsInLds && p.nsph <= kDeepLvMaxSpheres) {
+      // (forward fold: no level slots, so no LDS for them and the occupancy the registers allow)
+      if (!kForwardFold && kLevelsInLds && p.nsph <= kDeepLvMaxSpheres) {
         launch_fast_lds<B, true, true>(p, grid, s);
       } else {
         launch_fast_lds<B, true, false>(p, grid, s);

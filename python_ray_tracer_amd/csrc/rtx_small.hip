@@ -17,13 +17,15 @@ hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEve
 }
 
 // the (lvl, stats) instantiations launch_fast_b can request for a scene below kTreeMinSpheres: its
-// table always fits the LDS beside the level slots (levels_in_lds), DEEP keeps every level in LDS
-// (S <= kDeepLvMaxSpheres)
+// table always fits the LDS beside the level slots (levels_in_lds); a DEEP kernel kept every level in
+// LDS (S <= kDeepLvMaxSpheres) before the forward fold
 template <int B, bool DEEP>
 hipError_t go_b(bool lvl, bool stats, bool img, const void* params, dim3 grid, uint32_t lds, hipStream_t s,
                 hipEvent_t e0, hipEvent_t e1) {
-  constexpr bool kLvl = DEEP ? kLevelsInLds : levels_in_lds<B, true, false>();
-  static_assert(!DEEP || kDeepLvMaxSpheres >= kTreeMinSpheres, "small DEEP scenes keep their levels in LDS");
+  // (the forward fold keeps no levels: DEEP kernels too run without level slots)
+  constexpr bool kLvl = DEEP ? (kLevelsInLds && !kForwardFold) : levels_in_lds<B, true, false>();
+  static_assert(!DEEP || kForwardFold || kDeepLvMaxSpheres >= kTreeMinSpheres,
+                "small DEEP scenes keep their levels in LDS");
   if (lvl != kLvl) return hipErrorInvalidValue;
   if (img) {  // image textures shaded in place: capped, counter-free launches only
     if constexpr (DEEP) return hipErrorInvalidValue;
