@@ -1872,14 +1872,17 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         cg = __builtin_fma(thr, lg_, cg);
         cb = __builtin_fma(thr, lb_, cb);
       }
-      if (DEEP && weighted && k >= B && !at_cap) {  // the chain goes on beyond this kernel's levels
+      // a DEEP launch goes on to its record level (the first pass: level B; the continuation pass:
+      // kDeepLevel3, the registers holding nothing per level), then defers the chain with a record
+      const int kmax = DEEP ? p.drec_level - kb : B;
+      if (DEEP && weighted && k >= kmax && !at_cap) {  // the chain goes on beyond this launch's levels
         deferred = true;
         appended = true;
-        rays_through = hits_through = kb + B;
+        rays_through = hits_through = kb + kmax;
         const int64_t slot = append_deferred(p, deferred_entry(p.mode == 2 || !TREE ? i : pixel_index(lane_id_fresh()),
-                                                               p.frame, kb + B, kb + B));
-        if (p.drec && slot >= 0 && slot < p.rec_cap && kb + B == p.drec_level) {
-          double* rec = p.drec + slot * rec_words(kb + B);
+                                                               p.frame, kb + kmax, kb + kmax));
+        if (p.drec && slot >= 0 && slot < p.rec_cap) {
+          double* rec = p.drec + slot * rec_words(kb + kmax);
           double rx = dx, ry = dy, rz = dz;
           reflect_dir(rx, ry, rz, s.nx, s.ny, s.nz);
           rec[0] = s.qx; rec[1] = s.qy; rec[2] = s.qz;
@@ -1889,7 +1892,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         }
         break;
       }
-      if (!weighted || k >= B || at_cap) break;
+      if (!weighted || k >= kmax || at_cap) break;
       thr = (thr * 0.5) * s.g;  // the reflection's weight, (R * 0.5) * g (shader.py:106)
     } else if (!weighted || k >= B || at_cap) {
       // terminal level: the reflection is black (capped: R = 0) or multiplied by zero
@@ -2780,7 +2783,8 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     double* const recs[2] = {rec2, (double*)(p.ws + lay.rec3)};
     const int levels[2] = {kDeepLevel2, kDeepLevel3};
     const int64_t caps[2] = {records_for(n_all, p.max_bounces, 1), records_for(n_all, p.max_bounces, 2)};
-    for (int pass = 0; pass < 2; ++pass) {
+    // (forward fold: one continuation pass goes on from level kDeepLevels + 1 to kDeepLevel3)
+    for (int pass = kForwardFold ? 1 : 0; pass < 2; ++pass) {
       Params q = p;
       q.mode = 2;
       q.n_tiles_x = q.n_tiles_y = 0;
