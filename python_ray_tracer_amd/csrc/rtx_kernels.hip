@@ -233,8 +233,14 @@ constexpr int kRecLevelWords = 5;
 __host__ __device__ constexpr int rec_words(int level) {
   return kForwardFold ? 10 : 6 + kRecLevelWords * (level + 1);
 }
+// the first DEEP pass's record level (forward fold: a runtime level, no storage per level; A/B r5zo
+// on unbounded renders end to end, 5 / 9 / 14 levels: C2 98.7 / 93.7 / 77.8 us, C3 378 / 367 / 326 us,
+// C4 2,514 / 2,485 / 2,440 us)
+constexpr int kFirstPassLevels = 14;
 constexpr int kDeepLevel2 = 2 * kDeepLevels + 1;  // deferral level of the first continuation pass
 constexpr int kDeepLevel3 = 3 * kDeepLevels + 2;  // ... and of the second
+static_assert(!kForwardFold || (kFirstPassLevels >= kDeepLevels && kFirstPassLevels < kDeepLevel3),
+              "first-pass record level");
 static_assert(kDeepLevel3 + 2 < kLevelMask, "deferred-entry level fields hold 7 bits");
 // Resume-record capacities per deferral level (pass 0: the first pass's level kDeepLevels;
 // 1, 2: the continuation passes'): at least 2^18 / 2^16 / 2^14, or one per 32 / 256 / 2048 pixels,
@@ -2759,7 +2765,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     p.dlist = list1;
     p.dcount = hdr + RTX_WS_COUNT;
     p.drec = capped ? nullptr : rec1;
-    p.drec_level = kDeepLevels;
+    p.drec_level = kForwardFold ? kFirstPassLevels : kDeepLevels;
     prof_mark(0, s);
     if (capped) {
       launch_fast(p.max_bounces, p, grid, s);
@@ -2773,7 +2779,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.in_list = list1;
   p.in_count = hdr + RTX_WS_COUNT;
   p.in_rec = capped ? nullptr : rec1;
-  p.in_level = kDeepLevels;
+  p.in_level = kForwardFold ? kFirstPassLevels : kDeepLevels;
   if (!capped && p.n_frames == 1) {
     // continuation passes: chains deferred for depth go on for kDeepLevels + 1 more levels in
     // the register-resident kernel, twice; ties and what is still alive after them go to the
