@@ -235,10 +235,11 @@ __host__ __device__ constexpr int rec_words(int level) {
 }
 // the first DEEP pass's record level (forward fold: a runtime level, no storage per level; A/B r5zo
 // on unbounded renders end to end, 5 / 9 / 14 levels: C2 98.7 / 93.7 / 77.8 us, C3 378 / 367 / 326 us,
-// C4 2,514 / 2,485 / 2,440 us)
-constexpr int kFirstPassLevels = 14;
+// C4 2,514 / 2,485 / 2,440 us; r5zp, 14 / 16 / 30 with the continuation pass to 60: C2 77.8 / 77.5 /
+// 77.4, C3 327 / 310 / 304, C4 2,437 / 2,380 / 2,166 us)
+constexpr int kFirstPassLevels = 30;
 constexpr int kDeepLevel2 = 2 * kDeepLevels + 1;  // deferral level of the first continuation pass
-constexpr int kDeepLevel3 = 3 * kDeepLevels + 2;  // ... and of the second
+constexpr int kDeepLevel3 = kForwardFold ? 60 : 3 * kDeepLevels + 2;  // ... and of the second (forward: the one)
 static_assert(!kForwardFold || (kFirstPassLevels >= kDeepLevels && kFirstPassLevels < kDeepLevel3),
               "first-pass record level");
 static_assert(kDeepLevel3 + 2 < kLevelMask, "deferred-entry level fields hold 7 bits");
