@@ -10,7 +10,10 @@ unclipped colour left in HBM (float32 [3, W*H]). PNG encoding is not part of a s
 Default workload: BASELINE.json configs[1] — the README scene at 1920x1080, 3 reflection bounces.
 ``--mode frames`` (the default at every N, weak scaling): every rank renders whole frames, no
 collective in the loop (the frame sharding of config C5), so N=1 and N>1 lines measure
-the same code path and output format. ``--mode tiles`` (strong scaling): every rank renders its
+the same code path and output format. Rank r renders frame r of a camera path through the config's
+camera (``scenes.rank_frame_spec``): rank 0 the config's own frame, so the N = 1 line is unchanged,
+and N ranks render N distinct frames per step. The top-level ``strong_scaling`` object is the
+row-tiled C4 frame (below) with its measured speed-up over one GPU and its gather per link. ``--mode tiles`` (strong scaling): every rank renders its
 interleaved row tile of ONE frame and the uint8 tiles are gathered to rank 0 (RCCL) every step; the
 default line carries it at every N as ``secondary.tiles_u8`` (the config) and ``secondary.c4_tiles``
 (C4, 7680x4320), on a one-rank process group at N=1.
@@ -145,6 +148,7 @@ def main():
         return
 
     F = max(1, args.frames_per_step)
+    own = scene  # the frame this rank renders (frames mode, F = 1)
     if args.mode == "frames" and F > 1:
         # rank r renders orbit frames r*F .. r*F+F-1 of a 256-frame orbit (C5 camera path)
         batch = [scenes.build_scene(scenes.with_camera(spec, scenes.orbit_position(rank * F + f, 256)))
@@ -154,10 +158,15 @@ def main():
             return r.render_batch(batch, out="u8" if args.out == "u8" else None)
         px_per_step = W * H * F * world
     elif args.mode == "frames":
+        # rank r renders frame r of the camera path through the config's camera (scenes.rank_frame_spec):
+        # rank 0 the config's frame itself (the N = 1 line), every other rank a distinct frame, so the
+        # N-GPU line renders N different frames per step and moves nothing between GPUs
+        own = scene if rank == 0 else scenes.build_scene(frame_spec_for_rank(spec, rank))
+
         def step():
             if args.out == "u8":
-                return r.render_tile(scene, out="u8")
-            return r.raytrace_scene(scene.camera.position, r.get_ray_directions(scene.camera), scene)
+                return r.render_tile(own, out="u8")
+            return r.raytrace_scene(own.camera.position, r.get_ray_directions(own.camera), own)
         px_per_step = W * H * world
     else:
         # strong scaling: every rank renders its interleaved row tile of ONE frame into a gather
@@ -225,7 +234,7 @@ def main():
         rs.render_batch(batch)
         n_px_launch = W * H * F
     elif args.mode == "frames" or world == 1:
-        rs.render_tile(scene)
+        rs.render_tile(own)
         n_px_launch = W * H
     else:
         from python_ray_tracer_amd.tiling import n_local_rows
@@ -304,7 +313,12 @@ def main():
                 "C5": "16 random spheres 1920x1080 seed 0"}[args.config]
                 + (", unbounded bounces" if B is None else f", {B} bounces"),
                 "width": W, "height": H, "max_bounces": B, "spheres": S, "output": args.out,
-                "mode": args.mode, "frames_per_step": F, "parallelism": f"{args.mode}x{world}"},
+                "mode": args.mode, "frames_per_step": F, "parallelism": f"{args.mode}x{world}",
+                "frames": ("one frame per rank and step: rank r renders frame r of the camera path through the "
+                           "config's camera (scenes.rank_frame_spec; rank 0 the config's frame)")
+                if args.mode == "frames" and F == 1 else
+                ("rank r renders orbit frames r*F .. r*F+F-1 of the 256-frame C5 orbit in one launch"
+                 if args.mode == "frames" else "one frame row-tiled over the ranks")},
             "roofline": {
                 "bound": "valu",
                 "kernel": f"k_render_fast<{B}>" if B is not None and B <= 6 else "k_render_fast<5, DEEP> (first pass)",
@@ -354,6 +368,9 @@ def main():
         }
         if secondary:
             line["secondary"] = secondary
+            ss = strong_scaling(secondary, world)
+            if ss:
+                line["strong_scaling"] = ss
         if cpu:
             line["gpu_vs_cpu"] = round(value / cpu["value"], 1)
             if cpu.get("single_core"):
@@ -365,6 +382,14 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def frame_spec_for_rank(spec: dict, rank: int) -> dict:
+    """The frame a rank renders in frames mode at one frame per step (tests/test_distributed_cpu.py
+    checks, over a gloo world of 2, that the ranks' frames differ and rank 0's is the config's)."""
+    from python_ray_tracer_amd import scenes
+
+    return scenes.rank_frame_spec(spec, rank)
 
 
 def tiles_stepper(r, scene, world, row_block, out, loopback=False, comm_reserve=None, rows=None, timed=False):
@@ -488,23 +513,23 @@ def secondary_tiles(args, r, scene, world, dev, coll_dev):
                                         "itself over RCCL, then assembled)" if loop else "")}
         if getattr(getattr(step, "tg", None), "timed", False):
             out["c4_tiles"]["gather"] = gather_timing(step.timing(), world, loop)
-        if world > 1:
-            # the strong-scaling speed-up in the same run: rank 0 alone renders the whole C4 frame
-            # as the one-rank tiles path does (straight into the uint8 frame), the others wait
-            if dist.get_rank() == 0:
-                c4 = scenes.build_scene(c4spec)
-                buf = torch.empty((4320, 7680, 3), dtype=torch.uint8, device=dev)
-                for _ in range(2):
-                    r4.render_tile(c4, out="u8", into=buf)
-                torch.cuda.synchronize(dev)
-                t0 = time.perf_counter()
-                for _ in range(k4):
-                    r4.render_tile(c4, out="u8", into=buf)
-                torch.cuda.synchronize(dev)
-                t1 = (time.perf_counter() - t0) / k4
-                out["c4_tiles"]["single_gpu_ms_per_step"] = round(t1 * 1e3, 5)
-                out["c4_tiles"]["speedup_vs_1gpu"] = round(t1 / (t / k4), 4)
-            dist.barrier()
+        # the strong-scaling speed-up in the same run: rank 0 alone renders the whole C4 frame
+        # as the one-rank tiles path does (straight into the uint8 frame), the others wait (at
+        # N = 1 the ratio is the loopback plan's overhead over the plain frame)
+        if dist.get_rank() == 0:
+            c4 = scenes.build_scene(c4spec)
+            buf = torch.empty((4320, 7680, 3), dtype=torch.uint8, device=dev)
+            for _ in range(2):
+                r4.render_tile(c4, out="u8", into=buf)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(k4):
+                r4.render_tile(c4, out="u8", into=buf)
+            torch.cuda.synchronize(dev)
+            t1 = (time.perf_counter() - t0) / k4
+            out["c4_tiles"]["single_gpu_ms_per_step"] = round(t1 * 1e3, 5)
+            out["c4_tiles"]["speedup_vs_1gpu"] = round(t1 / (t / k4), 4)
+        dist.barrier()
     except Exception as e:  # noqa: BLE001
         if world > 1:
             # N > 1: the row-tiled frame is the north star's multi-GPU mechanism; a broken plan must
@@ -532,16 +557,47 @@ def gather_timing(mine: dict, world: int, loop: bool) -> dict:
     g = {"part_bytes": root["part_bytes"], "root_gather_ms": round(root["gather_ms"], 4),
          "root_assemble_ms": round(root["assemble_ms"], 4), "root_received_bytes": root["bytes"]}
     if loop:
-        g["link"] = "loopback: RCCL send/recv to the same GPU (HBM to HBM), not an xGMI link"
+        # HBM to HBM on one GPU: never an xGMI figure
+        g["link"] = "loopback (HBM)"
         g["loopback_GBps"] = round(root["part_bytes"] / max(root["gather_ms"], 1e-6) / 1e6, 2)
+        g["xgmi_GBps_per_peer"] = None
     else:
         peers = [a["gather_ms"] for a in allt[1:]]
         g["link"] = "xGMI point-to-point, one peer per link into the root"
         g["peer_send_ms"] = [round(x, 4) for x in peers]
-        g["link_GBps_per_peer"] = [round(root["part_bytes"] / max(x, 1e-6) / 1e6, 2) for x in peers]
-        g["link_GBps_min"] = min(g["link_GBps_per_peer"]) if peers else None
+        g["xgmi_GBps_per_peer"] = [round(root["part_bytes"] / max(x, 1e-6) / 1e6, 2) for x in peers]
+        g["xgmi_GBps_min"] = min(g["xgmi_GBps_per_peer"]) if peers else None
         g["root_in_GBps"] = round(root["bytes"] / max(root["gather_ms"], 1e-6) / 1e6, 2)
     return g
+
+
+# The xGMI rate DESIGN.md §6's 1 -> 8 prediction assumes for RCCL point-to-point traffic (per link and
+# direction). The one place it lives: a bench line that measured the gather over xGMI reports the
+# measured rate beside it (strong_scaling.gather.xgmi_GBps_min), which replaces it.
+ASSUMED_XGMI_GBPS = 40.0
+
+
+def strong_scaling(secondary: dict | None, world: int) -> dict | None:
+    """The row-tiled C4 frame (the north star's multi-GPU mechanism) at the top level of the line:
+    its throughput, the whole frame rendered by rank 0 alone in the same run, the speed-up, and the
+    gather per peer (bytes, ms, GB/s per link). From ``secondary.c4_tiles``; None without it."""
+    c4 = (secondary or {}).get("c4_tiles")
+    if not c4:
+        return None
+    out = {"config": c4["config"], "n_gpus": world, "value": c4["value"], "unit": c4["unit"],
+           "ms_per_step": c4["ms_per_step"], "single_gpu_ms_per_step": c4.get("single_gpu_ms_per_step"),
+           "speedup_vs_1gpu": c4.get("speedup_vs_1gpu"),
+           "note": "speedup_vs_1gpu = rank 0 rendering the whole C4 frame alone / the row-tiled frame over "
+                   "n_gpus ranks with its RCCL gather, both in this run (N = 1: a loopback plan, the "
+                   "ratio is the gather path's overhead)"}
+    g = c4.get("gather")
+    if g:
+        out["gather"] = g
+        measured = g.get("xgmi_GBps_min")
+        out["xgmi_GBps"] = {"measured": measured, "assumed": None if measured else ASSUMED_XGMI_GBPS,
+                            "note": "DESIGN.md §6 predicts the 1 -> 8 curve from the assumed rate until a "
+                                    "run over xGMI measures it"}
+    return out
 
 
 def emulate_parts(args, r, scene, spec, B, part_counts):

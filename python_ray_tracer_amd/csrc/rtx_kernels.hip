@@ -2582,11 +2582,13 @@ WsLayout ws_layout(int64_t n, int max_bounces) {
   const int64_t nrec3 = records_for(n, max_bounces, 2);
   w.fetch = RTX_WS_HDR_BYTES;
   w.list1 = w.fetch + (size_t)kMaxFetch * kFetchStride * sizeof(uint32_t);
+  // (forward fold: the first continuation pass, list 2 and its records, is never launched — run_render
+  // starts at the second — so they take no bytes; ADVICE r5: 275 MB of the unbounded C4 workspace)
   w.list2 = w.list1 + round256(list_bytes(n));
-  w.list3 = w.list2 + (nrec ? round256(list_bytes(n)) : 0);
+  w.list3 = w.list2 + (nrec && !kForwardFold ? round256(list_bytes(n)) : 0);
   w.rec1 = w.list3 + (nrec ? round256(list_bytes(n)) : 0);
   w.rec2 = w.rec1 + round256((size_t)nrec * rec_words(kDeepLevels) * sizeof(double));
-  w.rec3 = w.rec2 + round256((size_t)nrec2 * rec_words(kDeepLevel2) * sizeof(double));
+  w.rec3 = w.rec2 + (kForwardFold ? 0 : round256((size_t)nrec2 * rec_words(kDeepLevel2) * sizeof(double)));
   w.stack = w.rec3 + round256((size_t)nrec3 * rec_words(kDeepLevel3) * sizeof(double));
   w.total = w.stack + (size_t)workers_for(n, max_bounces) * stack_levels_for(max_bounces) * kFrameWords * 8;
   return w;

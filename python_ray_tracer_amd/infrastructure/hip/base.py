@@ -235,7 +235,7 @@ class HipRenderer(Renderer):
         # False defers those pixels to the general kernel (same colours)
         self.fast_textures = bool(fast_textures)
         self._ws = None
-        self._graph_pins: list = []  # tensors a captured launch points at (_tile_launch)
+        self._graph_pins: dict = {}  # data_ptr -> tensor a captured launch points at (_tile_launch)
         self.stats_buffer = torch.zeros(L.S_WORDS, dtype=torch.int64, device=self.device) if collect_stats else None
 
     # ---------------------------------------------------------------- plumbing
@@ -408,9 +408,19 @@ class HipRenderer(Renderer):
         if torch.cuda.is_current_stream_capturing():
             # a captured launch keeps raw pointers to the blob, the workspace and the learnt order:
             # pin them for the renderer's life, so that a cache eviction (scene cache, workspace
-            # growth, the 64-key order cache) cannot free memory a graph replay reads
-            self._graph_pins.extend(t for t in (blob, ws, order) if t is not None)
+            # growth, the 64-key order cache) cannot free memory a graph replay reads.
+            # Keyed by address, so recapturing the same scene pins nothing new; release_graph_pins()
+            # drops them once the caller has dropped its graphs
+            self._graph_pins.update((t.data_ptr(), t) for t in (blob, ws, order) if t is not None)
         return blob, n_spheres, rows, ws, flags, probe, key, order, cost
+
+    def release_graph_pins(self) -> int:
+        """Forget the tensors pinned for graph replays (``_tile_launch``). Call it after dropping
+        every CUDA graph captured from this renderer: a replay after it may read freed memory.
+        Returns how many tensors were released."""
+        n = len(self._graph_pins)
+        self._graph_pins.clear()
+        return n
 
     def _sched_plan(self, key, width, rows, n_spheres):
         """(tile_order, tile_cost) of a camera launch (rtx_render_camera_sched). The launch hands

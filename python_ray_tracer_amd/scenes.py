@@ -130,6 +130,27 @@ def orbit_position(frame: int, n_frames: int = 256) -> list:
     return [math.sin(theta), 0.2, -2.0 - math.cos(theta)]
 
 
+def path_position(spec: dict, frame: int, n_frames: int = 256) -> list:
+    """Frame k of the camera path through a config's own camera (the ``bench.py --gpus N``
+    headline: rank r renders frame r, so frame 0 — rank 0, and the N = 1 line — is the config's
+    frame itself). A circle of radius 1 in the horizontal plane, frame 0 at the camera and the
+    centre one unit behind it: (cx + sin θ, cy, cz - 1 + cos θ), θ = 2πk/n. z stays ≤ cz, so a
+    config camera in front of the reference's fixed screen (z < 0, ``base.py:131-141``) stays there."""
+    cx, cy, cz = (float(v) for v in spec["camera"]["position"])
+    theta = 2.0 * math.pi * frame / n_frames
+    return [cx + math.sin(theta), cy, (cz - 1.0) + math.cos(theta)]
+
+
+def rank_frame_spec(spec: dict, rank: int, n_frames: int = 256) -> dict:
+    """The frame a rank of the weak-scaling headline renders: the config's own spec at rank 0
+    (unchanged, so the N = 1 line is the single-GPU line), frame ``rank`` of ``path_position``
+    elsewhere — every rank a distinct frame of one camera path, as ``render_image_pipeline`` renders
+    one frame per call (``application.py:43-52``)."""
+    if rank % n_frames == 0:
+        return spec
+    return with_camera(spec, path_position(spec, rank, n_frames))
+
+
 def with_camera(spec: dict, position=None, width=None, height=None) -> dict:
     """Copy of ``spec`` with camera fields replaced."""
     out = copy.deepcopy(spec)

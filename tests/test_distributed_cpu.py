@@ -14,10 +14,15 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from pathlib import Path
+
 from oracle import numpy_oracle as O
 from python_ray_tracer_amd import scenes, tiling
 from python_ray_tracer_amd.application import render_frame_distributed, render_frames
 from python_ray_tracer_amd.distributed import TileGather
+
+
+REPO = Path(__file__).resolve().parent.parent
 
 
 class OracleTileRenderer:
@@ -125,6 +130,53 @@ def test_row_tiles_gather_equals_single_frame(world, row_block):
         assert set().union(*shards) == set(range(8))
         for r in range(world):
             assert shards[r] == {k for k in range(8) if k % world == r}
+
+
+def _headline_worker(rank, world, port, outdir):
+    """One rank of the bench headline at N = world (frames mode, one frame per step): the frame
+    bench.py picks for this rank, rendered by the oracle at a small size, its hash gathered."""
+    import hashlib
+    import sys
+
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        spec, B = scenes.CONFIGS["C2"]()
+        small = scenes.with_camera(spec, width=48, height=27)
+        mine = bench.frame_spec_for_rank(small, rank)
+        img = O.render(O.scene_from_spec(mine), B)
+        got = [None] * world
+        dist.all_gather_object(got, (mine["camera"]["position"], hashlib.sha256(img.tobytes()).hexdigest()))
+        if rank == 0:
+            np.save(os.path.join(outdir, "rank0.npy"), img)
+            with open(os.path.join(outdir, "ranks.txt"), "w") as f:
+                f.write(repr(got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_headline_ranks_render_distinct_frames():
+    """at N > 1 the frames-mode headline renders a different frame on every rank
+    (frame r of the camera path through the config's camera), and rank 0's frame is the N = 1
+    line's (the config's own frame), so SCALE's N = 1 point equals BENCH."""
+    import ast
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_headline_worker, args=(world, _free_port(), d), nprocs=world, start_method="spawn",
+                           join=True)
+        got = ast.literal_eval(open(os.path.join(d, "ranks.txt")).read())
+        spec, B = scenes.CONFIGS["C2"]()
+        small = scenes.with_camera(spec, width=48, height=27)
+        assert got[0][0] == small["camera"]["position"]
+        assert got[0][0] != got[1][0] and got[0][1] != got[1][1]  # distinct cameras and images
+        assert np.array_equal(np.load(os.path.join(d, "rank0.npy")), O.render(O.scene_from_spec(small), B))
+    # the path stays in front of the reference's fixed screen (z < 0) for all 256 frames
+    assert all(scenes.path_position(spec, k)[2] <= spec["camera"]["position"][2] for k in range(256))
 
 
 def test_default_shares():

@@ -81,6 +81,26 @@ def test_1080p_B3_full_size(hip, golden_meta, tag):
     assert np.array_equal(got32, got.astype(np.float32))
 
 
+# The colour drift the kernel's reassociations introduce ("Where the kernel departs from
+# the reference's association": the forward fold and the fused shading sums) measured over every golden
+# case and both 1080p goldens: the worst |GPU - reference| must stay at or below this ceiling, well
+# under the 1e-12 parity bar, so that a regression towards the bar shows here first.
+DRIFT_CEIL = 2e-13
+
+
+def test_reassociation_drift_is_pinned(hip, golden_meta, golden_renders):
+    worst = {}
+    for name, case in golden_meta["cases"].items():
+        _, got = _render(hip, case["spec"], case["max_bounces"])
+        worst[name] = float(np.abs(got - golden_renders[name]).max())
+    for tag in ("main", "readme"):
+        spec = golden_meta[f"ref_1080p_B3_{tag}"]["spec"]
+        _, got = _render(hip, spec, 3)
+        worst[f"1080p_B3_{tag}"] = float(np.abs(got - O.render(O.scene_from_spec(spec), 3)).max())
+    print("max |gpu - reference| per golden:", json.dumps(worst))
+    assert max(worst.values()) <= DRIFT_CEIL, worst
+
+
 def test_ties_take_the_general_kernel(hip, golden_meta, golden_renders):
     case = golden_meta["cases"]["ties_64x36_B2"]
     r, got = _render(hip, case["spec"], 2, stats=True)
@@ -379,6 +399,36 @@ def test_unbounded_recursion_limit(hip):
     scene = scenes.build_scene(spec)
     with pytest.raises(RecursionError):
         r.render(scene)
+
+
+@pytest.mark.parametrize("cap", [61, 80])
+def test_deep_chains_resume_past_levels_30_and_60(hip, cap):
+    """every chain deterministically outlives both resume records of the uncapped
+    pipeline and then ends. Rays trapped in a negative-radius mirror sphere (camera and light at its
+    centre: every hit lit, g = 1) reflect until the cap, so each pixel is deferred by the first DEEP
+    pass with its 10-word record at level 30 (kFirstPassLevels), continued from rin[6..9] by the
+    continuation pass to its level-60 record (kDeepLevel3), and finished by the general kernel
+    resuming from that record (cap 80: levels 61-80; cap 61: the single level past the record).
+    Colour, uint8 and the per-level ray/hit counters (levels 0-63) against the oracle."""
+    spec = scenes.readme_spec(24, 16)
+    spec["spheres"] = [{"center": [0, 0.2, -2], "radius": -5.0,
+                        "shader": {"reflection_gain": 1, "specular_gain": 1.0, "specular_roughness": 0.5,
+                                   "iridescence_gain": 0.05, "diffuse_gain": 0.5,
+                                   "texture": {"kind": "const", "color": [0.9, 0.7, 0.4]}}}]
+    spec["lights"][0]["position"] = [0, 0.2, -2]
+    osc = O.scene_from_spec(spec)
+    st = O.TraceStats()
+    want = O.render(osc, cap, stats=st)
+    assert len(st.rays) == cap + 1 and st.rays[31] == st.rays[61] == 24 * 16  # every chain passes 31 and 61
+    r = hip.HipRenderer(max_bounces=cap, color_dtype=torch.float64)
+    got = r.render(scenes.build_scene(spec)).data.cpu().numpy()
+    assert np.abs(got - want).max() <= ATOL, (cap, np.abs(got - want).max())
+    assert np.array_equal(O.to_uint8(got, 24, 16), O.to_uint8(want, 24, 16))
+    rs = hip.HipRenderer(max_bounces=cap, collect_stats=True)
+    rs.render(scenes.build_scene(spec))
+    s = rs.stats()
+    n = min(len(st.rays), hip._lib.S_LEVELS)
+    assert s["rays"][:n] == st.rays[:n] and s["hits"][:n] == st.hits[:n]
 
 
 def _fuzz_spec(seed):

@@ -17,6 +17,7 @@
 #   emul:C           bench.py --emulate-parts 2,4,8 for config C
 #   tiles:C          bench.py --mode tiles --loopback for config C (the RCCL gather path on one GPU)
 #   fuzz:N:SEED      tools/fuzz_parity.py over N random scenes from SEED
+#   repro:VARIANT    tools/capture_repro VARIANT (RCCL under graph capture; memcpy|plain|fork|stale)
 #   ab:ARGS          tools/ab.py with ARGS (comma-separated, e.g. ab:--config,C2,--variants,base,x)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -86,6 +87,10 @@ for step in "$@"; do
       n=${arg%%:*}
       seed=${arg#*:}
       run "fuzz_$seed" 500 python -u tools/fuzz_parity.py --n "$n" --seed0 "$seed" --out "$O/fuzz_$seed.json" ;;
+    repro)
+      # tools/capture_repro.cpp variant ARG over torch's librccl and HIP runtime (the crash's setting)
+      TL=$(python -c "import torch, os; print(os.path.dirname(torch.__file__) + '/lib')")
+      LD_LIBRARY_PATH=$TL run "repro_$arg" 60 tools/capture_repro "$arg" "$TL/librccl.so" ;;
     ab)
       run "ab_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40)" 900 python -u tools/ab.py $(echo "$arg" | tr ',' ' ') ;;
     *)
