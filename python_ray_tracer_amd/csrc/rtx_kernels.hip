@@ -1418,14 +1418,18 @@ __device__ __forceinline__ void nearest_masked(const P* geo, uint64_t m0, uint64
 // The wave's active rays (O, D) leave from a ball around the first active lane's origin Oc, of
 // radius rho >= |O - Oc|, in directions within angle theta of that lane's direction A
 // (1 - cos theta >= 1 - D.A in every lane). A point X = O + tD (t > 0) within R' of a centre C puts
-// Oc + tD within R'' = R' + rho of it, so D lies within phi = asin(R'' / |C - Oc|) of W = C - Oc and
-// A within theta + phi: cos(A, W) >= cos(theta + phi) = cos theta cos phi - sin theta sin phi
-// (theta, phi <= 90 degrees). With R' = r + lm (the culling margin of wave_frustum, doubled again:
-// scale over the whole ball, |C - O| <= |W| + rho and |O| <= |Oc| + rho), a sphere failing that
-// test (and not reaching the ball itself) yields FARAWAY for every ray of the wave, so the nearest
-// hit (and the tie flag) over the others is unchanged. rho^2 and 1 - cos theta are bounded by
-// powers of two found by ballots (a binary search over the active lanes' exponents, exact under any
-// exec mask), so no cross-lane arithmetic is needed. Comparisons keep the sphere on NaN.
+// Oc + tD within R = R' + rho of it, so D lies within phi = asin(R / |W|) of W = C - Oc and A
+// within theta + phi: A.W >= |W| cos(theta + phi) = cos theta sqrt(|W|^2 - R^2) - sin theta R
+// (theta, phi <= 90 degrees). With R' = r + lm (the culling margin of wave_frustum, doubled again and
+// taken over the whole ball: |C - O|^2 <= 2|W|^2 + 2 rho^2, |O|^2 <= 2|Oc|^2 + 2 rho^2), a sphere
+// failing that test (and not reaching the ball itself) yields FARAWAY for every ray of the wave, so
+// the nearest hit (and the tie flag) over the others is unchanged. The test is evaluated squared,
+// without a square root of |W|^2 - R^2 (round 6): with t1 = A.W + sin theta R (plus an absolute
+// slack for its rounding), a sphere is dropped when t1 < 0 (the right side is >= 0) or when
+// t1^2 < (|W|^2 - R^2) cos^2 theta, the difference lowered by its rounding bound and the product
+// by a relative 1e-12, so every rounding keeps the sphere. rho^2 and 1 - cos theta are bounded by
+// powers of two, the wave maxima of the lanes' exponents (wave_max_jump: exact under any exec mask,
+// no cross-lane arithmetic). Comparisons keep the sphere on NaN.
 // Only the active lanes run here (the bounce loop's lanes leave it one by one), so the spheres are
 // dealt out by rank: the active lane of rank k tests spheres k, k + n, k + 2n (n active lanes), and
 // pass j's ballot holds sphere j n + rank(lane) at the lane's bit. False (take the culling tree)
@@ -1433,6 +1437,11 @@ __device__ __forceinline__ void nearest_masked(const P* geo, uint64_t m0, uint64
 // than 2^6 or the candidates more than kBeamMaxCand.
 constexpr int kBeamPasses = 3;
 constexpr int kBeamMaxCand = 24;
+// The beam kernels stage, in the LDS copy of the sphere table, each sphere's own part of the test's
+// radius in geometry word RTX_G_IDX (unused in the main table): r (bounded above) plus the margin's
+// per-sphere terms, beam_word below. The per-lane test then needs no square root of its own.
+constexpr bool kBeamStaged = true;
+static_assert(RTX_GEOM_WORDS == 8 && RTX_G_IDX == 7, "beam word: the last geometry word");
 struct Beam {
   uint64_t m[kBeamPasses];  // pass j: candidate bits at the testing lanes' positions
   uint64_t ex;              // the active lanes
@@ -1445,17 +1454,18 @@ __device__ __forceinline__ double rfl_d(double x) {
   const int lo = __builtin_amdgcn_readfirstlane(__double2loint(x));
   return __hiloint2double(hi, lo);
 }
-// max over the active lanes of v in [lo, hi] (binary search by ballots)
-__device__ __forceinline__ int wave_max_int(int v, int lo, int hi) {
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (__ballot(v >= mid) != 0) {
-      lo = mid;
-    } else {
-      hi = mid - 1;
-    }
+// Max over the active lanes of a small int v: start from the last active lane's value and jump to
+// a larger value some lane holds until no lane holds one (exact under any exec mask; one or two
+// ballots for the nearby origins and directions of a wave tile, where the binary search of rounds
+// 3-5 took seven and six).
+__device__ __forceinline__ int wave_max_jump(int v) {
+  const uint64_t ex = __ballot(1);
+  int cur = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(ex));
+  for (;;) {
+    const uint64_t b = __ballot(v > cur);
+    if (b == 0) return cur;
+    cur = __builtin_amdgcn_readlane(v, __builtin_ctzll(b));
   }
-  return lo;
 }
 // e with x < 2^e for x in [0, 2^hi): exponents below lo report lo; NaN and anything larger hi + 1
 __device__ __forceinline__ int pow2_above(double x, int lo, int hi) {
@@ -1464,16 +1474,20 @@ __device__ __forceinline__ int pow2_above(double x, int lo, int hi) {
   const int e = __builtin_amdgcn_frexp_exp(x);  // x = m 2^e, m in [0.5, 1)
   return e < lo ? lo : e;
 }
-// sqrt for the beam's culling test: the hardware reciprocal square root and two Newton steps
-// (relative error far below 1e-13; the callers scale by 1 -+ 1e-13 towards keeping the sphere).
-// 0 and inf give NaN, which the test's comparisons read as "keep the sphere".
+// sqrt for the beam's culling test: the hardware reciprocal square root (~2^-24 relative) and one
+// Newton step (~1e-15 relative: quadratic in the estimate's error); callers scale by 1 + 1e-11
+// towards keeping the sphere. 0 and inf give NaN, which the test's comparisons read as "keep".
 __device__ __forceinline__ double sqrt_cull(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
-  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
-  return x * y;
+  const double y = __builtin_amdgcn_rsq(x);
+  return x * (y * __builtin_fma(-0.5 * x * y, y, 1.5));
 }
-template <typename T>
+// r (bounded above) + 4e-7 (2 C.C + 3 r^2) (1 + 1e-12): the sphere's own part of R (the same sum as
+// wave_beam's unstaged R, reassociated; the test's outer 1 + 1e-12 covers the reassociation)
+__device__ __forceinline__ double beam_word(double cc, double rr) {
+  return sqrt_cull(rr) * (1.0 + 1e-11) + 4e-7 * ((2.0 * cc + 3.0 * rr) * (1.0 + 1e-12));
+}
+// STAGED: tab is the LDS copy whose word RTX_G_IDX holds beam_word (k_render_fast's staging loop)
+template <bool STAGED, typename T>
 __device__ __forceinline__ bool wave_beam(const T* tab, int nb, double ox, double oy, double oz, double dx,
                                           double dy, double dz, Beam& bm) {
   bm.ex = __ballot(1);
@@ -1484,29 +1498,37 @@ __device__ __forceinline__ bool wave_beam(const T* tab, int nb, double ox, doubl
   const double Ox = rfl_d(ox), Oy = rfl_d(oy), Oz = rfl_d(oz);
   const double Ax = rfl_d(dx), Ay = rfl_d(dy), Az = rfl_d(dz);
   const double wox = ox - Ox, woy = oy - Oy, woz = oz - Oz;
-  const int er = wave_max_int(pow2_above((wox * wox + woy * woy) + woz * woz, -60, 12), -60, 13);
+  const int er = wave_max_jump(pow2_above((wox * wox + woy * woy) + woz * woz, -60, 12));
   const double omc = 1.0 - ((dx * Ax + dy * Ay) + dz * Az);
-  const int ea = wave_max_int(pow2_above(omc, -60, -1), -60, 0);
+  const int ea = wave_max_jump(pow2_above(omc, -60, -1));
   if (er > 12 || ea > -1) return false;
-  const double rho = __builtin_sqrt(__builtin_ldexp(1.0, er)) * (1.0 + 1e-12);
-  const double ct = 1.0 - __builtin_ldexp(1.0, ea);                                 // <= cos theta
-  const double st = __builtin_sqrt(__builtin_ldexp(1.0, ea + 1)) * (1.0 + 1e-12);   // >= sin theta
-  const double om = __builtin_sqrt((Ox * Ox + Oy * Oy) + Oz * Oz) + rho;          // >= |O|
+  const double rho2 = __builtin_ldexp(1.0, er);                 // > |O - Oc|^2 in every lane
+  const double rho = sqrt_cull(rho2) * (1.0 + 1e-11);            // >= its square root
+  const double ct = 1.0 - __builtin_ldexp(1.0, ea);              // <= cos theta (>= 1/2)
+  const double ct2 = (ct * ct) * (1.0 - 1e-12);                  // <= cos^2 theta
+  const double st = sqrt_cull(__builtin_ldexp(1.0, ea + 1)) * (1.0 + 1e-11);  // >= sin theta
+  // the margin's terms common to every sphere: 2 rho^2 of |C - O|^2 and the bound on |O|^2
+  const double lmk = ((2.0 * rho2 + 2.0 * ((Ox * Ox + Oy * Oy) + Oz * Oz)) + 2.0 * rho2) + 1.0;
   const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm.ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm.ex, 0));
   auto may = [&](int s) {
     if (s >= nb) return false;
     const T* e = tab + s * RTX_GEOM_WORDS;
     const double wx = e[RTX_G_CX] - Ox, wy = e[RTX_G_CY] - Oy, wz = e[RTX_G_CZ] - Oz;
-    const double rr = e[RTX_G_RR];
-    const double wq = sqrt_cull((wx * wx + wy * wy) + wz * wz);
-    const double w = wq * (1.0 - 1e-13);         // <= |W|
-    const double wr = wq * (1.0 + 1e-13) + rho;  // >= |W| + rho
-    const double lm = 4e-7 * ((((wr * wr + 2.0 * e[RTX_G_CC]) + 3.0 * rr) + om * om) + 1.0);
-    const double R = ((sqrt_cull(rr) * (1.0 + 1e-13) + lm) + rho) * (1.0 + 1e-12);
-    if (!(w > R)) return true;
+    const double ww = (wx * wx + wy * wy) + wz * wz;  // |W|^2
+    double R;
+    if constexpr (STAGED) {
+      R = ((e[RTX_G_IDX] + 4e-7 * ((2.0 * ww + lmk) * (1.0 + 1e-12))) + rho) * (1.0 + 1e-12);
+    } else {
+      const double rr = e[RTX_G_RR];
+      const double lm = 4e-7 * ((((2.0 * ww + 2.0 * e[RTX_G_CC]) + 3.0 * rr) + lmk) * (1.0 + 1e-12));
+      R = ((sqrt_cull(rr) * (1.0 + 1e-11) + lm) + rho) * (1.0 + 1e-12);
+    }
+    const double R2 = R * R;
+    if (!(ww > R2 * (1.0 + 1e-12))) return true;  // the ball may reach the sphere
     const double aw = (Ax * wx + Ay * wy) + Az * wz;
-    const double rhs = ct * (sqrt_cull((w - R) * (w + R)) * (1.0 - 1e-13)) - st * R;
-    return !(aw < rhs - 1e-9 * ((w + R) + 1.0));
+    const double t1 = (aw + st * R) + 1e-9 * ((ww + R2) + 2.0);  // (the slack: >= 1e-9 (|W| + R + 1))
+    if (t1 < 0.0) return false;
+    return !(t1 * t1 < (((ww - R2) - 1e-15 * (ww + R2)) * ct2));
   };
   int cand = 0;
 #pragma unroll
@@ -1952,7 +1974,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       // the wave's beam candidates (tame scenes up to 128 spheres), else the culling tree
       Beam bm;
       const double* btab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
-      if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam(btab, nb, ox, oy, oz, dx, dy, dz, bm)) {
+      if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam<kBeamStaged && LDS>(btab, nb, ox, oy, oz, dx, dy, dz, bm)) {
         if (st) stat_wave(st, RTX_S_BEAMW);
         for (int j = 0; j < bm.passes; ++j) {  // a lane's sphere test per pass, priced as two node tests
           wk.node();                            // (like wave_frustum)
@@ -2067,7 +2089,11 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
   if constexpr (LDS) {  // per-lane view of the sphere table: one LDS copy per block (the barrier is
                         // in fast_tile, after the first tile's level-0 nearest-hit test)
     const double* src = p.scene + RTX_HDR_WORDS;
-    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += fast_block<TREE>()) lds_tab[k] = src[k];
+    for (int k = threadIdx.x; k < p.nsph * kSphWords; k += fast_block<TREE>()) {
+      // (the beam kernels: geometry word RTX_G_IDX of the copy holds beam_word, see wave_beam)
+      const bool bw = BEAM && kBeamStaged && k < p.nsph * RTX_GEOM_WORDS && (k & (RTX_GEOM_WORDS - 1)) == RTX_G_IDX;
+      lds_tab[k] = bw ? beam_word(src[k - RTX_G_IDX + RTX_G_CC], src[k - RTX_G_IDX + RTX_G_RR]) : src[k];
+    }
   }
   if constexpr (DEEP) {
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride

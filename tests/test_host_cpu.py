@@ -583,18 +583,22 @@ def _beam_candidates(G, Oc, A, r2, omc, drop_rho=False):
     er, ea = int(p2above(r2, -60, 12).max()), int(p2above(omc, -60, -1).max())
     if er > 12 or ea > -1:
         return None
-    rho = 0.0 if drop_rho else np.sqrt(2.0 ** er) * (1 + 1e-12)
-    ct, st = 1 - 2.0 ** ea, np.sqrt(2.0 ** (ea + 1)) * (1 + 1e-12)
-    om = np.sqrt(Oc @ Oc) + rho
+    # the kernel's bounds (round 6: the test squared, no square root of |W|^2 - R^2; sqrt_cull is
+    # within ~1e-15 of the square root, the callers' 1 + 1e-11 keeps every bound on the safe side)
+    rho2 = 0.0 if drop_rho else 2.0 ** er
+    rho = np.sqrt(rho2) * (1 + 1e-11)
+    ct = 1 - 2.0 ** ea
+    ct2, st = (ct * ct) * (1 - 1e-12), np.sqrt(2.0 ** (ea + 1)) * (1 + 1e-11)
+    lmk = ((2 * rho2 + 2 * (Oc @ Oc)) + 2 * rho2) + 1.0
     Wv = G[:, :3] - Oc
-    wq = np.sqrt((Wv ** 2).sum(1))
-    w = wq * (1 - 1e-13)  # the kernel's bounds around its approximate square roots (sqrt_cull)
+    ww = (Wv ** 2).sum(1)
     rr, CC = G[:, 3] ** 2, (G[:, :3] ** 2).sum(1)
-    lm = 4e-7 * ((((wq * (1 + 1e-13) + rho) ** 2 + 2 * CC) + 3 * rr) + om * om + 1)
-    R = (np.sqrt(rr) * (1 + 1e-13) + lm + rho) * (1 + 1e-12)
-    with np.errstate(invalid="ignore"):
-        rhs = ct * (np.sqrt((w - R) * (w + R)) * (1 - 1e-13)) - st * R
-    return ~(w > R) | ~(Wv @ A < rhs - 1e-9 * ((w + R) + 1))
+    lm = 4e-7 * ((((2 * ww + 2 * CC) + 3 * rr) + lmk) * (1 + 1e-12))
+    R = ((np.sqrt(rr) * (1 + 1e-11) + lm) + rho) * (1 + 1e-12)
+    R2 = R * R
+    t1 = (Wv @ A + st * R) + 1e-9 * ((ww + R2) + 2.0)
+    drop = (ww > R2 * (1 + 1e-12)) & ((t1 < 0) | (t1 * t1 < ((ww - R2) - 1e-15 * (ww + R2)) * ct2))
+    return ~drop
 
 
 @pytest.mark.parametrize("seed", [0, 3])

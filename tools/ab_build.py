@@ -3,11 +3,12 @@
     python tools/ab_build.py OUT.so [--set kName=VALUE ...] [--rev GIT_REV] [--patch FILE.py]
 
 The shipped kernel has no tuning macros: its tuning values are ``constexpr`` lines in
-``csrc/rtx_kernels.hip``. A variant rewrites those lines (``--set kLvWaves=4``), takes the source of
-another revision (``--rev HEAD~3``: the baseline of an A/B), or applies named patches of the A/B
-patch set (``--patch tile_trace,nogen``: ``tools/ab_patches.py``) or a Python file defining
-``patch(src: str) -> str``, and compiles it with the library's own flags next to the original (so
-its relative #include resolves).
+``csrc/rtx_kernels.hip``. A variant rewrites those lines (``--set kFwdWavesPersist=5``), takes the
+source of another revision (``--rev HEAD~3``: the baseline of an A/B), or applies a Python file
+defining ``patch(src: str) -> str``, and compiles it with the library's own flags next to the
+original (so its relative #include resolves). (Rounds 2-5 kept a set of named source patches,
+tools/ab_patches.py; round 6 retired it with the experiments it served, whose results are in
+profiles/ and DESIGN.md, and which stay in git history.)
 """
 
 import argparse
@@ -47,8 +48,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--set", action="append", default=[], help="kName=VALUE (a constexpr tuning line)")
     ap.add_argument("--rev", default=None, help="git revision of csrc/rtx_kernels.hip to build")
-    ap.add_argument("--patch", default=None,
-                    help="comma list of tools/ab_patches.py names, or a python file defining patch(src) -> src")
+    ap.add_argument("--patch", default=None, help="a python file defining patch(src) -> src")
     ap.add_argument("--flag", action="append", default=[], help="extra hipcc flag")
     ap.add_argument("--small-flag", action="append", default=None,
                     help="hipcc flag of the small-scene unit only (replaces _build.SMALL_FLAGS)")
@@ -68,13 +68,8 @@ def main():
         src, n = pat.subn(lambda m: m.group(1) + val + m.group(3), src)
         if n != 1:
             raise SystemExit(f"--set {name}: {n} matching constexpr lines")
-    if a.patch and a.patch.endswith(".py"):
+    if a.patch:
         src = runpy.run_path(a.patch)["patch"](src)
-    elif a.patch:
-        sys.path.insert(0, str(REPO / "tools"))
-        import ab_patches
-
-        src = ab_patches.apply(src, a.patch)
     if a.only_b is not None:
         src = trim(src, {int(b) for b in a.only_b.split(",") if b})
     tmp = _build.SRC.with_name(f"_ab_{Path(a.out).stem}.hip")

@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
   printf("graph nodes: %zu\n", nodes);
   STEP("hipGraphInstantiate", hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   for (int k = 0; k < 2; ++k) {
-    STEP("hipMemset", hipMemset(rb, 0, n));
+    STEP("hipMemsetAsync", hipMemsetAsync(rb, 0, n, s));  // (on s: the graph's stream is non-blocking)
     STEP("hipGraphLaunch", hipGraphLaunch(ge, s));
     STEP("hipStreamSynchronize", hipStreamSynchronize(s));
     STEP("hipMemcpy D2H", hipMemcpy(back.data(), rb, n, hipMemcpyDeviceToHost));

@@ -1,4 +1,5 @@
-"""profiles/pmc_traffic.json from a tools/gpu_pmc.sh session: HBM bytes per k_render_fast launch
+"""profiles/pmc_traffic.json from the ``pmc:C`` steps of a tools/session.sh session (before round 6:
+tools/gpu_pmc.sh, in git history): HBM bytes per k_render_fast launch
 per config (median over the timed instantiation's dispatches; FETCH_SIZE x2 + WRITE_SIZE, the
 calibration of profiles/r2_traffic_calibration.txt), which bench.py reports as roofline.traffic.
 

@@ -50,7 +50,7 @@ for step in "$@"; do
   case $kind in
     tests)
       if [ -n "$arg" ]; then
-        run "pytest_gpu_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_')" 900 python -u -m pytest tests -m gpu -x -v \
+        run "pytest_gpu_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_')" 900 python -u -m pytest tests -m gpu -x -v -rP \
           -p no:cacheprovider --timeout 120 --timeout-method thread -k "$arg"
       else
         run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
