@@ -1665,13 +1665,15 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // instantiations compile none of it.
 // IMG: image-textured spheres are shaded here (the texel lookup compiled in, RTX_F_IMAGES launches)
 // instead of deferred to the general kernel.
-template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM, bool IMG = false>
+// NSPH > 0: the scene has exactly NSPH spheres, a compile-time count (the timed small-scene kernels,
+// rtx_small.hip: their sphere loops unroll; A/B r6b, C2 -2.7%); 0: p.nsph at run time.
+template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM, bool IMG = false, int NSPH = 0>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   constexpr int FB = fast_block<TREE>();  // threads per block of this instantiation
   const cdouble* sc = (const cdouble*)p.scene;
   const cdouble* geo = sc + RTX_HDR_WORDS;
-  const int nsph = p.nsph;
+  const int nsph = NSPH > 0 ? NSPH : p.nsph;
   const int nb = TREE ? huge_tail(sc, nsph) : nsph;  // the beams' tested spheres
   // the half-b sphere test (SphTest): origins the kernel generates itself, in a tame scene
   const double tame = p.mode != 1 && p.mode != 3 && sc[RTX_H_TAME] != 0.0 ? 0x1.0p-350 : __builtin_nan("");
@@ -2064,7 +2066,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 // TP: 0 = no culling tree and no persistent launch (scenes below kTreeMinSpheres), 1 = culling tree,
 // one tile per block (the launch is not persistent), 2 = both (persistent launches)
 template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2,
-          bool IMG = false>
+          bool IMG = false, int NSPH = 0>
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
                              (DEEP  ? kDeepWaves
                               : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
@@ -2081,7 +2083,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     // sized by p.nsph): render nothing and flag it (block-uniform, so the persistent launch's
     // fetch counters stay untouched)
     const cdouble* sc = (const cdouble*)p.scene;
-    if (sc[RTX_H_MAGIC] != RTX_MAGIC || sc[RTX_H_NSPH] != (double)p.nsph) {
+    if (sc[RTX_H_MAGIC] != RTX_MAGIC || sc[RTX_H_NSPH] != (double)p.nsph || (NSPH > 0 && p.nsph != NSPH)) {
       if (threadIdx.x == 0) atomicOr((uint32_t*)p.ws + RTX_WS_STATUS, (uint32_t)RTX_ST_BAD_SCENE);
       return;
     }
@@ -2099,7 +2101,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
       const int64_t count = (int64_t)*p.in_count;
       for (int64_t t = blockIdx.x; t * fast_block<TREE>() < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
+        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG, NSPH>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
       }
       return;
     }
@@ -2141,7 +2143,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
         // instantiations (run_render picks one for a launch that records them): in the timed kernel
         // the record costs C4 six more spilled VGPRs and 2.5% (A/B r4h)
         if (STATS && p.tile_cost && lane == 0) p.tile_cost[t] = 0u - (uint32_t)__builtin_amdgcn_s_memrealtime();
-        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false,
+        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG, NSPH>(p, t - row * p.n_tiles_x, p.n_tiles_y - 1 - row, false,
                                                               lds_tab, true);
         if (STATS && p.tile_cost && lane == 0) atomicAdd(p.tile_cost + t, (uint32_t)__builtin_amdgcn_s_memrealtime());
       }
@@ -2168,7 +2170,7 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
     bx = tb % gridDim.x;
     by = gridDim.y - 1 - tb / gridDim.x;
   }
-  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG>(p, bx, by, true, lds_tab);
+  fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG, NSPH>(p, bx, by, true, lds_tab);
   if (STATS && p.tile_cost && (threadIdx.x & 63) == 0)  // the block's time: the slowest of its waves
     atomicMax(p.tile_cost + tb, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_entry));
 }

@@ -8,12 +8,31 @@
 
 namespace {
 
-template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false>
+template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false, int NSPH = 0>
 hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const Params& p = *static_cast<const Params*>(params);
-  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0, IMG>), grid, dim3(fast_block<false>()), lds, s, e0,
-                        e1, 0u, p);
+  hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0, IMG, NSPH>), grid, dim3(fast_block<false>()), lds,
+                        s, e0, e1, 0u, p);
   return hipSuccess;  // launch errors reach the caller's check_launch through hipGetLastError
+}
+
+// The kernels without counters or image textures (the timed capped ones and the DEEP ones of
+// unbounded renders) of each sphere count below kTreeMinSpheres, with the count a compile-time
+// constant (fast_tile's NSPH: the sphere loops unroll; A/B r6b, C2 -2.7%); the counter and
+// texturing kernels keep the run-time count.
+template <int B, bool DEEP, bool LVL>
+hipError_t go_ns(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  static_assert(kTreeMinSpheres == 8, "one instantiation per sphere count 1..7");
+  switch (static_cast<const Params*>(params)->nsph) {
+    case 1: return go<B, DEEP, LVL, false, false, 1>(params, grid, lds, s, e0, e1);
+    case 2: return go<B, DEEP, LVL, false, false, 2>(params, grid, lds, s, e0, e1);
+    case 3: return go<B, DEEP, LVL, false, false, 3>(params, grid, lds, s, e0, e1);
+    case 4: return go<B, DEEP, LVL, false, false, 4>(params, grid, lds, s, e0, e1);
+    case 5: return go<B, DEEP, LVL, false, false, 5>(params, grid, lds, s, e0, e1);
+    case 6: return go<B, DEEP, LVL, false, false, 6>(params, grid, lds, s, e0, e1);
+    case 7: return go<B, DEEP, LVL, false, false, 7>(params, grid, lds, s, e0, e1);
+    default: return go<B, DEEP, LVL, false>(params, grid, lds, s, e0, e1);
+  }
 }
 
 // the (lvl, stats) instantiations launch_fast_b can request for a scene below kTreeMinSpheres: its
@@ -32,7 +51,7 @@ hipError_t go_b(bool lvl, bool stats, bool img, const void* params, dim3 grid, u
     else return stats ? hipErrorInvalidValue : go<B, DEEP, kLvl, false, true>(params, grid, lds, s, e0, e1);
   }
   return stats ? go<B, DEEP, kLvl, true>(params, grid, lds, s, e0, e1)
-               : go<B, DEEP, kLvl, false>(params, grid, lds, s, e0, e1);
+               : go_ns<B, DEEP, kLvl>(params, grid, lds, s, e0, e1);
 }
 
 }  // namespace

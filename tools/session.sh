@@ -18,6 +18,7 @@
 #   tiles:C          bench.py --mode tiles --loopback for config C (the RCCL gather path on one GPU)
 #   fuzz:N:SEED      tools/fuzz_parity.py over N random scenes from SEED
 #   repro:VARIANT    tools/capture_repro VARIANT (RCCL under graph capture; memcpy|plain|fork|stale)
+#   capture:VARIANT  tools/capture_tiles.py VARIANT (a gathering tiles plan under graph capture)
 #   ab:ARGS          tools/ab.py with ARGS (comma-separated, e.g. ab:--config,C2,--variants,base,x)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -53,7 +54,7 @@ for step in "$@"; do
         run "pytest_gpu_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_')" 900 python -u -m pytest tests -m gpu -x -v -rP \
           -p no:cacheprovider --timeout 120 --timeout-method thread -k "$arg"
       else
-        run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+        run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rP -p no:cacheprovider --timeout 120 \
           --timeout-method thread
       fi ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
@@ -91,6 +92,9 @@ for step in "$@"; do
       # tools/capture_repro.cpp variant ARG over torch's librccl and HIP runtime (the crash's setting)
       TL=$(python -c "import torch, os; print(os.path.dirname(torch.__file__) + '/lib')")
       LD_LIBRARY_PATH=$TL run "repro_$arg" 60 tools/capture_repro "$arg" "$TL/librccl.so" ;;
+    capture)
+      # tools/capture_tiles.py ARG: a gathering tiles plan captured into a HIP graph (native backtrace on a crash)
+      run "capture_$arg" 120 python -u tools/capture_tiles.py "$arg" ;;
     ab)
       run "ab_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40)" 900 python -u tools/ab.py $(echo "$arg" | tr ',' ' ') ;;
     *)
