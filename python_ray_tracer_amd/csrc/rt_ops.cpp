@@ -12,6 +12,10 @@
 //   rt::assemble_rows <- the multi-GPU frame's row un-permute (application.render_frame_distributed),
 //                        equal shares or weighted ones (root_run / run: rtx_assemble_runs)
 //   rt::status        <- reads and clears the workspace's sticky RTX_ST_* flags
+//   rt::comm_unique_id, rt::comm_init, rt::comm_destroy, rt::tiles_create, rt::tiles_submit,
+//   rt::tiles_finish, rt::tiles_destroy
+//                     <- the row-tiled multi-GPU frame of render_frame_distributed, one native call
+//                        per frame and rank (rtx_tiles_*: render, RCCL gather to the root, assembly)
 //   rt::workspace_bytes
 //
 // Conventions (those of a TORCH_CHECKed op): tensors must live on the GPU, be contiguous and have
@@ -380,6 +384,100 @@ int64_t workspace_bytes(int64_t n_rays, int64_t max_bounces) {
   return (int64_t)rtx_workspace_bytes(n_rays, (int)max_bounces);
 }
 
+// ---- the row-tiled multi-GPU frame (rtx_tiles_*, rtx_comm_*; csrc/rtx_tiles.hip) ---------------
+// Handles are plain int64: a communicator from comm_init, a plan from tiles_create. The caller keeps
+// the plan's buffers (send / recv, the workspace, the frame) alive until tiles_destroy, as the C ABI
+// asks. These are what distributed.TileGather drives through ctypes; an integrator binding only the
+// ops gets the same overlapped native gather.
+
+void* as_ptr(int64_t h) { return reinterpret_cast<void*>(static_cast<intptr_t>(h)); }
+int64_t as_handle(void* p) { return static_cast<int64_t>(reinterpret_cast<intptr_t>(p)); }
+
+struct DeviceScope {  // the current device set to `device` (>= 0) for the scope
+  int prev = -1;
+  explicit DeviceScope(int64_t device) {
+    if (device >= 0) {
+      TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice failed");
+      TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice(", device, ") failed");
+    }
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+at::Tensor comm_unique_id() {
+  check_rc(rtx_rccl_load(nullptr), "rtx_rccl_load");
+  at::Tensor id = at::empty({128}, at::TensorOptions().dtype(at::kByte));
+  check_rc(rtx_comm_unique_id(id.data_ptr()), "rtx_comm_unique_id");
+  return id;
+}
+
+int64_t comm_init(const at::Tensor& unique_id, int64_t world, int64_t rank, int64_t device, int64_t max_ctas) {
+  TORCH_CHECK(!unique_id.is_cuda() && unique_id.scalar_type() == at::kByte && unique_id.numel() == 128 &&
+                  unique_id.is_contiguous(),
+              "unique_id must be the 128-byte host uint8 tensor comm_unique_id returned (broadcast to every rank)");
+  check_rc(rtx_rccl_load(nullptr), "rtx_rccl_load");
+  DeviceScope scope(device);
+  void* comm = nullptr;
+  check_rc(rtx_comm_init(unique_id.data_ptr(), (int)world, (int)rank, (int)max_ctas, &comm), "rtx_comm_init");
+  return as_handle(comm);
+}
+
+void comm_destroy(int64_t comm) { check_rc(rtx_comm_destroy(as_ptr(comm)), "rtx_comm_destroy"); }
+
+int64_t tiles_create(int64_t comm, int64_t world, int64_t rank, int64_t root, int64_t width, int64_t height,
+                     int64_t row_block, int64_t out_kind, int64_t slots, at::TensorList send, at::TensorList recv,
+                     int64_t part_bytes, int64_t root_run, int64_t run, int64_t flags, int64_t device) {
+  TORCH_CHECK(slots >= 1 && slots <= RTX_TILES_MAX_SLOTS, "slots must be in 1..", RTX_TILES_MAX_SLOTS);
+  TORCH_CHECK(send.empty() || (int64_t)send.size() == slots, "send: one buffer per slot, or none");
+  TORCH_CHECK(recv.empty() || (int64_t)recv.size() == slots, "recv: one buffer per slot, or none");
+  std::vector<void*> sp, rp;
+  for (const at::Tensor& t : send) {
+    check_gpu(t, "send buffer", at::kByte);
+    TORCH_CHECK(t.numel() >= part_bytes, "a send buffer must hold part_bytes");
+    sp.push_back(t.data_ptr());
+  }
+  for (const at::Tensor& t : recv) {
+    check_gpu(t, "recv buffer", at::kByte);
+    TORCH_CHECK(t.numel() >= world * part_bytes, "a recv buffer must hold world * part_bytes");
+    rp.push_back(t.data_ptr());
+  }
+  DeviceScope scope(device);
+  void* plan = nullptr;
+  check_rc(rtx_tiles_create(as_ptr(comm), (int)world, (int)rank, (int)root, (int)width, (int)height, (int)row_block,
+                            (int)out_kind, (int)slots, sp.empty() ? nullptr : sp.data(),
+                            rp.empty() ? nullptr : rp.data(), part_bytes, (int)root_run, (int)run,
+                            (unsigned)flags, &plan),
+           "rtx_tiles_create");
+  return as_handle(plan);
+}
+
+void tiles_submit(int64_t plan, int64_t slot, const at::Tensor& scene, int64_t n_spheres, int64_t max_bounces,
+                  at::Tensor& workspace, const std::optional<at::Tensor>& frame, int64_t flags) {
+  check_scene(scene, n_spheres);
+  const at::OptionalDeviceGuard guard(at::device_of(scene));
+  check_bounces(max_bounces);
+  check_gpu(workspace, "workspace", at::kByte);
+  check_same_device(scene, workspace, "workspace");
+  if (frame) {
+    TORCH_CHECK(frame->is_cuda() && frame->is_contiguous(), "frame must be a contiguous GPU tensor");
+    check_same_device(scene, *frame, "frame");
+  }
+  check_rc(rtx_tiles_submit(as_ptr(plan), (int)slot, scene.data_ptr<double>(), (int)n_spheres, (int)max_bounces,
+                            workspace.data_ptr(), (size_t)workspace.numel(), (unsigned)flags, nullptr, nullptr,
+                            nullptr, frame ? frame->data_ptr() : nullptr, stream_of(scene)),
+           "rtx_tiles_submit");
+}
+
+void tiles_finish(int64_t plan, int64_t slot, int64_t device) {
+  TORCH_CHECK(device >= 0, "tiles_finish needs the plan's device index");
+  check_rc(rtx_tiles_finish(as_ptr(plan), (int)slot, c10::hip::getCurrentHIPStream((int)device).stream()),
+           "rtx_tiles_finish");
+}
+
+void tiles_destroy(int64_t plan) { check_rc(rtx_tiles_destroy(as_ptr(plan)), "rtx_tiles_destroy"); }
+
 // ---- fake (Meta) kernels: output shapes only, for tracing (torch.compile / FakeTensor) ----------
 
 at::Tensor render_tile_meta(const at::Tensor& scene, int64_t n_spheres, int64_t width, int64_t height,
@@ -444,6 +542,19 @@ TORCH_LIBRARY(rt, m) {
         "int run=1) -> Tensor");
   m.def("status(Tensor(a!) workspace) -> int");
   m.def("workspace_bytes(int n_rays, int max_bounces) -> int", &workspace_bytes);
+  // the row-tiled multi-GPU frame (one native call per frame and rank; handles are int64)
+  m.def("comm_unique_id() -> Tensor", &comm_unique_id);
+  m.def("comm_init(Tensor unique_id, int world, int rank, int device=-1, int max_ctas=0) -> int", &comm_init);
+  m.def("comm_destroy(int comm) -> ()", &comm_destroy);
+  m.def("tiles_create(int comm, int world, int rank, int root, int width, int height, int row_block, int out_kind, "
+        "int slots, Tensor[] send, Tensor[] recv, int part_bytes, int root_run=1, int run=1, int flags=0, "
+        "int device=-1) -> int",
+        &tiles_create);
+  m.def("tiles_submit(int plan, int slot, Tensor scene, int n_spheres, int max_bounces, Tensor(a!) workspace, "
+        "Tensor(b!)? frame=None, int flags=0) -> ()",
+        &tiles_submit);
+  m.def("tiles_finish(int plan, int slot, int device) -> ()", &tiles_finish);
+  m.def("tiles_destroy(int plan) -> ()", &tiles_destroy);
 }
 
 TORCH_LIBRARY_IMPL(rt, CUDA, m) {

@@ -55,7 +55,10 @@ from python_ray_tracer_amd.infrastructure.hip import _lib
 OPS_LIB = Path(__file__).resolve().parent / "librt_ops.so"
 RTX_LIB = Path(__file__).resolve().parent / "librtx_hip.so"  # what librt_ops.so links by $ORIGIN
 OPS = ("render_tile", "render_frames", "trace", "shade_hits", "intersect", "quantize_u8", "assemble_rows",
-       "status", "workspace_bytes")
+       "status", "workspace_bytes",
+       # the row-tiled multi-GPU frame (rtx_tiles_*: render, RCCL gather, assembly in one native call)
+       "comm_unique_id", "comm_init", "comm_destroy", "tiles_create", "tiles_submit", "tiles_finish",
+       "tiles_destroy")
 
 
 def load() -> None:

@@ -247,3 +247,47 @@ def test_ops_accept_inference_tensors(env):
             assert torch.equal(torch.ops.rt.render_tile(blob, S, 40, 23, 1, 1, 0, 3, 0, ws), want)
         with pytest.raises(RuntimeError, match="holds 3 spheres"):
             torch.ops.rt.render_tile(blob, S - 1, 40, 23, 1, 1, 0, 3, 0, ws)
+
+
+def test_tiles_plan_through_ops(env):
+    """The native row-tiled frame through the op surface alone (rt::comm_* / rt::tiles_*; VERDICT r5):
+    a one-rank direct plan (the tile is the frame, no communicator) and a one-rank loopback plan over
+    a communicator made by rt::comm_unique_id / rt::comm_init (the tile sent to and received from the
+    rank itself over RCCL, then assembled), two slots in flight; every frame equals
+    HipRenderer.render_tile's uint8 frame (application.py:43-52)."""
+    H = env
+    W, Hh, rb, B = 104, 57, 8, 4
+    base = scenes.random_spec(40, 2, W, Hh)
+    frames = [scenes.build_scene(scenes.with_camera(base, scenes.orbit_position(k, 9))) for k in range(4)]
+    r = H.HipRenderer(max_bounces=B, color_dtype=torch.float32)
+    want = [r.render_tile(sc, out="u8").clone() for sc in frames]
+    blobs = [r.scene_blob(sc) for sc in frames]
+    dev = torch.cuda.current_device()
+    ws = torch.zeros(torch.ops.rt.workspace_bytes(W * Hh, B), dtype=torch.uint8, device="cuda")
+    part = (W * Hh * 3 + 15) // 16 * 16
+    comm = torch.ops.rt.comm_init(torch.ops.rt.comm_unique_id(), 1, 0, dev)
+    try:
+        for loop in (False, True):
+            send = [torch.zeros(part, dtype=torch.uint8, device="cuda") for _ in range(2)] if loop else []
+            recv = [torch.zeros(part, dtype=torch.uint8, device="cuda") for _ in range(2)] if loop else []
+            plan = torch.ops.rt.tiles_create(comm if loop else 0, 1, 0, 0, W, Hh, rb, 2, 2, send, recv, part,
+                                             flags=1 if loop else 0, device=dev)  # 1: RTX_TILES_LOOPBACK
+            try:
+                out = [torch.empty((Hh, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+                got, open_slot = [], None
+                for k, (blob, S) in enumerate(blobs):
+                    slot = k % 2
+                    torch.ops.rt.tiles_submit(plan, slot, blob, S, B, ws, out[slot])
+                    if open_slot is not None:
+                        torch.ops.rt.tiles_finish(plan, open_slot, dev)
+                        got.append(out[open_slot].clone())
+                    open_slot = slot
+                torch.ops.rt.tiles_finish(plan, open_slot, dev)
+                got.append(out[open_slot].clone())
+                torch.cuda.synchronize()
+                for k in range(len(frames)):
+                    assert torch.equal(got[k], want[k]), (loop, k)
+            finally:
+                torch.ops.rt.tiles_destroy(plan)
+    finally:
+        torch.ops.rt.comm_destroy(comm)

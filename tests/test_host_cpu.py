@@ -387,6 +387,31 @@ def test_torch_ops_registered_and_checked_on_host():
         torch.ops.rt.status(ws)
 
 
+def test_tiles_ops_schema_and_host_checks():
+    """The native row-tiled frame through the op surface (rtx_tiles_* had no op): the
+    communicator and plan ops exist with int64 handles, mutate the workspace and frame they are given,
+    and refuse bad arguments on the host before anything is created or launched."""
+    import python_ray_tracer_amd.ops  # noqa: F401
+
+    sch = {n: str(getattr(torch.ops.rt, n).default._schema) for n in
+           ("comm_unique_id", "comm_init", "comm_destroy", "tiles_create", "tiles_submit", "tiles_finish",
+            "tiles_destroy")}
+    assert sch["comm_unique_id"].endswith("-> Tensor")
+    assert "Tensor unique_id, int world, int rank, int device=-1, int max_ctas=0) -> int" in sch["comm_init"]
+    assert "int slots, Tensor[] send, Tensor[] recv, int part_bytes, int root_run=1, int run=1, int flags=0" \
+        in sch["tiles_create"] and sch["tiles_create"].endswith("-> int")
+    assert "Tensor(a!) workspace, Tensor(b!)? frame=None, int flags=0) -> ()" in sch["tiles_submit"]
+    assert "int plan, int slot, int device" in sch["tiles_finish"]
+    with pytest.raises(RuntimeError, match="unique_id"):
+        torch.ops.rt.comm_init(torch.zeros(64, dtype=torch.uint8), 1, 0)
+    with pytest.raises(RuntimeError, match="slots"):
+        torch.ops.rt.tiles_create(0, 1, 0, 0, 8, 8, 1, 2, 0, [], [], 256)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.tiles_create(0, 2, 1, 0, 8, 8, 1, 2, 1, [torch.zeros(256, dtype=torch.uint8)], [], 256)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        torch.ops.rt.tiles_submit(0, 0, torch.zeros(200, dtype=torch.float64), 3, 3, torch.zeros(64, dtype=torch.uint8))
+
+
 def test_torch_ops_schema_and_fake_kernels():
     """The render ops declare their workspace and stats as mutated (Tensor(a!), Tensor(b!)?) and
     carry a check flag; every op has a Meta kernel returning the output a GPU call returns, so the

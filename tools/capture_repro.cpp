@@ -3,7 +3,7 @@
 // (python_ray_tracer_amd/csrc/rtx_tiles.hip). No torch, no renderer: one process, one GPU, a one-rank
 // communicator over the librccl given on the command line (torch's own, as in the crash).
 //
-//   hipcc -O2 -std=c++17 -o tools/capture_repro tools/capture_repro.cpp -ldl
+//   hipcc -x hip --offload-arch=gfx950 -O2 -std=c++17 -o tools/capture_repro tools/capture_repro.cpp -ldl
 //   tools/capture_repro VARIANT LIBRCCL
 //
 // VARIANT (each step is printed before it runs, so a crash names its call):
@@ -13,6 +13,9 @@
 //           back by another (rtx_tiles_submit + rtx_tiles_finish)
 //   stale   fork, plus, first, a wait of the capturing stream on an event recorded before the capture
 //           began (a reused slot's `done` event: rtx_tiles_submit's first call)
+//   kbefore fork, plus a kernel on the capturing stream before the fork (the render)
+//   kafter  fork, plus a kernel on the side stream after the RCCL group (the root's assembly)
+//   kboth   both kernels: the whole shape of rtx_tiles_submit + rtx_tiles_finish
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -21,6 +24,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+// a stand-in for the render (before the fork) and the assembly (after the RCCL group): one pass over
+// the buffer
+__global__ void touch(unsigned char* p, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = p[i];
+}
 
 #define STEP(what, call)                                                \
   do {                                                                  \
@@ -37,7 +47,7 @@
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s memcpy|plain|fork|stale LIBRCCL\n", argv[0]);
+    fprintf(stderr, "usage: %s memcpy|plain|fork|stale|kbefore|kafter|kboth LIBRCCL\n", argv[0]);
     return 1;
   }
   const char* v = argv[1];
@@ -92,6 +102,13 @@ int main(int argc, char** argv) {
     STEP("ncclRecv (capturing stream)", recv(rb, n, ncclUint8, 0, comm, s));
     STEP("ncclGroupEnd", gend());
   } else {
+    const bool kb = !strcmp(v, "kbefore") || !strcmp(v, "kboth"), ka = !strcmp(v, "kafter") || !strcmp(v, "kboth");
+    if (kb) {
+      printf("step: kernel on the capturing stream\n");
+      fflush(stdout);
+      hipLaunchKernelGGL(touch, dim3((unsigned)(n / 256)), dim3(256), 0, s, (unsigned char*)sb, n);
+      STEP("hipGetLastError", hipGetLastError());
+    }
     STEP("fork: record on the capturing stream", hipEventRecord(fork_ev, s));
     STEP("fork: side stream waits", hipStreamWaitEvent(cs, fork_ev, 0));
     if (!strcmp(v, "memcpy")) {
@@ -101,6 +118,12 @@ int main(int argc, char** argv) {
       STEP("ncclSend (side stream)", send(sb, n, ncclUint8, 0, comm, cs));
       STEP("ncclRecv (side stream)", recv(rb, n, ncclUint8, 0, comm, cs));
       STEP("ncclGroupEnd", gend());
+    }
+    if (ka) {
+      printf("step: kernel on the side stream after the group\n");
+      fflush(stdout);
+      hipLaunchKernelGGL(touch, dim3((unsigned)(n / 256)), dim3(256), 0, cs, (unsigned char*)rb, n);
+      STEP("hipGetLastError", hipGetLastError());
     }
     STEP("join: record on the side stream", hipEventRecord(join_ev, cs));
     STEP("join: capturing stream waits", hipStreamWaitEvent(s, join_ev, 0));

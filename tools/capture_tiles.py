@@ -5,10 +5,14 @@ way tests/test_gpu_distributed.py did at commit dd6da5d, with a native backtrace
 this script drives the plan's own entry point (HipRenderer.submit_tiles, what TileGather.submit
 calls) to reach the capture anyway.
 
-    python tools/capture_tiles.py VARIANT        (VARIANT: assembled | rows | fresh)
+    python tools/capture_tiles.py VARIANT        (VARIANT: assembled | rows | fresh | ops_torch | ops_raw)
 
 ``fresh``: the captured frame goes through a second plan whose slot has carried no frame, so
 rtx_tiles_submit does not wait on the slot's `done` event recorded before the capture began.
+``ops_torch`` / ``ops_raw``: no torch.distributed process group at all (no ProcessGroupNCCL
+communicator in the process): the loopback plan is made through the torch ops (rt::comm_init,
+rt::tiles_create) and captured by torch.cuda.graph, or by hipStreamBeginCapture/EndCapture called
+directly (ctypes on the process's libamdhip64).
 
 Prints one line per step, then "ok" with the replays' result; exits 139 with the backtrace on a
 segmentation fault. Run it in its own process (tools/session.sh capture:VARIANT).
@@ -29,8 +33,82 @@ def say(*a):
     print(*a, flush=True)
 
 
+def ops_variant(variant):
+    """A loopback plan through the torch ops, no process group; captured by torch or by raw HIP."""
+    import torch
+
+    import python_ray_tracer_amd.ops  # noqa: F401
+    from python_ray_tracer_amd import scenes
+    from python_ray_tracer_amd.infrastructure.hip import HipRenderer
+
+    dev = torch.cuda.current_device()
+    W, H, B = 96, 61, 3
+    sc = scenes.build_scene(scenes.random_spec(40, 6, W, H))
+    r = HipRenderer(max_bounces=B, color_dtype=torch.float32)
+    want = r.render_tile(sc, out="u8").clone()
+    blob, S = r.scene_blob(sc)
+    ws = torch.zeros(torch.ops.rt.workspace_bytes(W * H, B), dtype=torch.uint8, device="cuda")
+    part = (W * H * 3 + 15) // 16 * 16
+    comm = torch.ops.rt.comm_init(torch.ops.rt.comm_unique_id(), 1, 0, dev)
+    send = [torch.zeros(part, dtype=torch.uint8, device="cuda")]
+    recv = [torch.zeros(part, dtype=torch.uint8, device="cuda")]
+    plan = torch.ops.rt.tiles_create(comm, 1, 0, 0, W, H, 8, 2, 1, send, recv, part, flags=1, device=dev)
+    frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+    torch.ops.rt.tiles_submit(plan, 0, blob, S, B, ws, frame)
+    torch.ops.rt.tiles_finish(plan, 0, dev)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, want)
+    say("eager frame equal (ops, no process group)")
+    trace = REPO / "tools" / "libsegv_trace.so"
+    if trace.exists():
+        ctypes.CDLL(str(trace)).segv_trace_install()
+        say("segv trace handler installed")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    if variant == "ops_torch":
+        g = torch.cuda.CUDAGraph()
+        say("capture begin (torch.cuda.graph)")
+        with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+            torch.ops.rt.tiles_submit(plan, 0, blob, S, B, ws, frame)
+            torch.ops.rt.tiles_finish(plan, 0, dev)
+            say("  submitted and finished; capture_end next")
+        say("capture end")
+        replay = g.replay
+    else:
+        import os
+
+        hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))  # torch's (loaded)
+        graph, exe = ctypes.c_void_p(), ctypes.c_void_p()
+        sh = ctypes.c_void_p(s.cuda_stream)
+        say("capture begin (hipStreamBeginCapture, global mode)")
+        assert hip.hipStreamBeginCapture(sh, 0) == 0
+        with torch.cuda.stream(s):
+            torch.ops.rt.tiles_submit(plan, 0, blob, S, B, ws, frame)
+            torch.ops.rt.tiles_finish(plan, 0, dev)
+        say("  submitted and finished; hipStreamEndCapture next")
+        rc = hip.hipStreamEndCapture(sh, ctypes.byref(graph))
+        say(f"hipStreamEndCapture rc={rc}")
+        assert rc == 0
+        assert hip.hipGraphInstantiate(ctypes.byref(exe), graph, None, None, ctypes.c_size_t(0)) == 0
+        say("instantiated")
+
+        def replay():
+            assert hip.hipGraphLaunch(exe, sh) == 0
+    for k in range(3):
+        frame.zero_()
+        torch.cuda.synchronize()
+        replay()
+        torch.cuda.synchronize()
+        say(f"replay {k}: {'equal' if torch.equal(frame, want) else 'MISMATCH'}")
+    torch.ops.rt.tiles_destroy(plan)
+    torch.ops.rt.comm_destroy(comm)
+    say("ok")
+
+
 def main():
     variant = sys.argv[1] if len(sys.argv) > 1 else "assembled"
+    if variant.startswith("ops_"):
+        return ops_variant(variant)
     import torch
     import torch.distributed as dist
 
