@@ -219,9 +219,11 @@ class TileGather:
             raise RuntimeError(f"slot {slot} still has a frame in flight: finish() it first")
         if self.plan is not None:
             if (self.world > 1 or self.send) and torch.cuda.is_current_stream_capturing():
-                # RCCL traffic inside a HIP graph capture: capture_end segfaults on this image (ROCm
-                # 7.2, torch 2.10's librccl; session r5a), so a gathering plan is
-                # refused up front; a one-rank plan (no RCCL operation) captures and replays
+                # RCCL traffic inside a HIP graph capture: hipStreamEndCapture overflows the stack in
+                # torch's bundled HIP runtime (unbounded recursion over its per-stream capture lists;
+                # the trigger is the RCCL group, not the plan's fork/join: DESIGN.md §6, round 6), so a
+                # gathering plan is refused up front; a one-rank plan (no RCCL operation) captures and
+                # replays
                 raise RuntimeError("a gathering TileGather plan cannot be captured into a HIP graph "
                                    "(RCCL send/recv under stream capture); run it eagerly")
             frame = None

@@ -178,10 +178,11 @@ def test_native_tiles_loopback_and_graph_replay():
 
 
 def test_gathering_plan_refuses_graph_capture(monkeypatch):
-    """RCCL send/recv captured into a HIP graph crashes capture_end on this image (session r5a:
-    segfault in torch.cuda.graph's capture_end for a loopback plan), so TileGather refuses to submit
-    a gathering plan under stream capture with a RuntimeError instead; a one-rank plan without RCCL
-    traffic still captures (test_native_tiles_loopback_and_graph_replay)."""
+    """RCCL send/recv captured into a HIP graph crashes the end of the capture in this image (a stack
+    overflow in torch's bundled HIP runtime's hipStreamEndCapture, triggered by the RCCL group:
+    DESIGN.md §6, tools/capture_tiles.py), so TileGather refuses to submit a gathering plan under
+    stream capture with a RuntimeError instead; a one-rank plan without RCCL traffic still captures
+    (test_native_tiles_loopback_and_graph_replay)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import torch.distributed as dist

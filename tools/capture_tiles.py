@@ -57,8 +57,7 @@ def ops_variant(variant):
     torch.ops.rt.tiles_submit(plan, 0, blob, S, B, ws, frame)
     torch.ops.rt.tiles_finish(plan, 0, dev)
     torch.cuda.synchronize()
-    assert torch.equal(frame, want)
-    say("eager frame equal (ops, no process group)")
+    say(f"eager frame {'equal' if torch.equal(frame, want) else 'DIFFERS'} (ops, no process group)")
     trace = REPO / "tools" / "libsegv_trace.so"
     if trace.exists():
         ctypes.CDLL(str(trace)).segv_trace_install()

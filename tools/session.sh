@@ -11,13 +11,14 @@
 #   tests:EXPR       pytest -m gpu -k EXPR
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (bench.py with no flags: what the driver runs)
+#   bench2[:C]       bench.py at N = 2 over gloo, both ranks on the one GPU (the N > 1 code path)
 #   bench:C          bench line of config C (C1 C2 C2main C3 C4 C5), CPU baselines included
 #   rocprof:C        rocprofv3 --kernel-trace --stats of config C's timed bench (no secondary legs)
 #   pmc:C            the PMC passes of config C: FETCH_SIZE, WRITE_SIZE, SQ cycles, VALU mix (one pass each)
 #   emul:C           bench.py --emulate-parts 2,4,8 for config C
 #   tiles:C          bench.py --mode tiles --loopback for config C (the RCCL gather path on one GPU)
 #   fuzz:N:SEED      tools/fuzz_parity.py over N random scenes from SEED
-#   repro:VARIANT    tools/capture_repro VARIANT (RCCL under graph capture; memcpy|plain|fork|stale)
+#   repro:VARIANT[:BYTES]  tools/capture_repro VARIANT (RCCL under graph capture; memcpy|plain|fork|stale)
 #   capture:VARIANT  tools/capture_tiles.py VARIANT (a gathering tiles plan under graph capture)
 #   ab:ARGS          tools/ab.py with ARGS (comma-separated, e.g. ab:--config,C2,--variants,base,x)
 set -u
@@ -64,6 +65,12 @@ for step in "$@"; do
       else
         run bench_default 300 python bench.py --json-out "$O/bench_default.json"
       fi ;;
+    bench2)
+      # two ranks sharing the box's one GPU over gloo (bench.py --backend gloo): the N > 1 frames line
+      # (distinct frames per rank), strong_scaling and the tiles legs through the gloo path
+      run bench2_gloo 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --gpus 2 --backend gloo --config "${arg:-C2}" --steps 50 --warmup 5 \
+        --cpu-seconds 0 --json-out "$O/bench2_gloo.json" ;;
     rocprof)
       run "rocprof_$arg" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$arg" -o run -- \
         python3 bench.py $(bargs "$arg") --cpu-seconds 0 --no-secondary ;;
@@ -91,7 +98,10 @@ for step in "$@"; do
     repro)
       # tools/capture_repro.cpp variant ARG over torch's librccl and HIP runtime (the crash's setting)
       TL=$(python -c "import torch, os; print(os.path.dirname(torch.__file__) + '/lib')")
-      LD_LIBRARY_PATH=$TL run "repro_$arg" 60 tools/capture_repro "$arg" "$TL/librccl.so" ;;
+      v=${arg%%:*}
+      bytes=${arg#*:}
+      [ "$bytes" = "$arg" ] && bytes=""
+      LD_LIBRARY_PATH=$TL run "repro_${v}_${bytes:-1MiB}" 60 tools/capture_repro "$v" "$TL/librccl.so" $bytes ;;
     capture)
       # tools/capture_tiles.py ARG: a gathering tiles plan captured into a HIP graph (native backtrace on a crash)
       run "capture_$arg" 120 python -u tools/capture_tiles.py "$arg" ;;
