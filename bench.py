@@ -247,8 +247,11 @@ def main():
     flops = 15 * n_px_launch + 20 * S * (R_tr + R_sh) + 200 * R_sh
     # the same model over the work the fast kernel actually executed: its ray-sphere tests (the
     # culling tree skips most of the S per ray at C3/C4; the shadow loop stops at the first
-    # occluder) and its culling-node tests (~22 flops: 6 subtractions, 6 products, 10 min/max/compare)
-    flops_exec = 15 * n_px_launch + 20 * st["sphere_tests"] + 22 * st["node_tests"] + 200 * R_sh
+    # occluder), its culling-node tests (~22 flops: 6 subtractions, 6 products, 10 min/max/compare)
+    # and its reflected-ray beam tests (a lane's cone test of one sphere, round 6: 34 f64 operations
+    # and 3 compares, rtx_kernels.hip wave_beam; until round 5 priced as two node tests)
+    flops_exec = (15 * n_px_launch + 20 * st["sphere_tests"] + 22 * st["node_tests"] + 37 * st["beam_tests"]
+                  + 200 * R_sh)
     out_bytes = {"f32": 12, "f64": 24, "u8": 3}[args.out]
     alg_bytes = out_bytes * n_px_launch + 8 * len(r.scene_blob(scene)[0]) * F  # framebuffer write + scene read
     kern_avg_s = kern_ms / 1e3 / max(kern_n, 1)
@@ -340,16 +343,18 @@ def main():
                     "achieved": round(achieved_exec, 4), "frac": round(achieved_exec / PEAK_FP64_TFLOPS, 5),
                     "flops_per_launch": flops_exec, "sphere_tests": st["sphere_tests"],
                     "node_tests": st["node_tests"], "box_tests": st["box_tests"],
+                    "beam_tests": st["beam_tests"],
                     "sphere_tests_reference": S * (R_tr + R_sh),
                     "reflected_rays": {"sphere_tests": st["sphere_tests_reflected"],
                                        "node_tests": st["node_tests_reflected"],
-                                       "beam_searches": st["beam_searches"],
+                                       "beam_searches": st["beam_searches"], "beam_tests": st["beam_tests"],
                                        "wave_searches": sum(st["waves_traced"][1:])},
-                    "note": "15/primary ray + 20/ray-sphere test + 22/culling-node test + 200/shaded hit over the "
-                            "tests k_render_fast executed (kernel counters); node_tests prices the culling tree's "
-                            "box tests (box_tests) and, as node tests too, the shadow-grid lookups and beam passes (the "
-                            "level-0 tile candidates' image-plane box comparisons are not priced); `achieved` above prices every test the reference performs "
-                            "(S per ray), culled or not"},
+                    "note": "15/primary ray + 20/ray-sphere test + 22/culling-node test + 37/beam test + 200/shaded "
+                            "hit over the tests k_render_fast executed (kernel counters); node_tests counts the "
+                            "culling tree's box tests (box_tests) and, priced as node tests too, the shadow-grid "
+                            "lookups; beam_tests the reflected-ray cone tests, one per live lane and beam pass (the "
+                            "level-0 tile candidates' image-plane box comparisons are not priced); `achieved` above "
+                            "prices every test the reference performs (S per ray), culled or not"},
                 "lane_utilisation": {
                     "traced": [round(r / (64 * w), 4) if w else None for r, w in zip(st["rays"], st["waves_traced"])],
                     "shaded": [round(h / (64 * w), 4) if w else None for h, w in zip(st["hits"], st["waves_shaded"])],

@@ -192,7 +192,7 @@ enum {
   RTX_S_TESTS = 3,    /* ray-sphere tests executed by live lanes (fast kernel; culling skips most) */
   RTX_S_NODES = 4,    /* culling-node (box) tests executed by live lanes (fast kernel)            */
   RTX_S_TESTS1 = 5,   /* ... of them, the sphere tests of reflected rays' nearest-hit searches (levels >= 1) */
-  RTX_S_NODES1 = 6,   /* ... and their node tests (beam plane tests priced as two node tests a pass) */
+  RTX_S_NODES1 = 6,   /* ... and their node tests (the culling tree's box tests where the beam was not used) */
   RTX_S_BEAMW = 7,    /* reflected-ray searches served by the wave's beam candidates (waves x levels) */
   RTX_S_LEVELS = 64,  /* levels recorded                        */
   RTX_S_RAYS = 8,     /* [8 .. 8+64): rays traced per level     */
@@ -201,7 +201,9 @@ enum {
   RTX_S_WSHADE = 200, /* [200 .. 200+64): waves that shaded a level (any lane hit), fast kernel  */
   RTX_S_BOXES = 264,  /* of RTX_S_NODES, the culling tree's box tests (the rest are frustum-plane, shadow-grid
                          and beam work priced as node tests)                                       */
-  RTX_S_WORDS = 265
+  RTX_S_BEAMT = 265,  /* reflected-ray beam tests: one per live lane and beam pass (a lane's cone test of one
+                         sphere; round 6, counted apart from the node tests they used to be priced as) */
+  RTX_S_WORDS = 266
 };
 
 /* workspace: status words then deferred-ray list then per-worker frame stacks.

@@ -559,16 +559,19 @@ struct Work {
   __device__ __forceinline__ void test(int) {}
   __device__ __forceinline__ void node() {}
   __device__ __forceinline__ void box() {}
+  __device__ __forceinline__ void beam() {}
 };
 template <>
 struct Work<true> {
   uint32_t tests = 0, nodes = 0;
   uint32_t tests1 = 0, nodes1 = 0;  // of the nearest-hit searches of reflected rays (levels >= 1)
-  uint32_t boxes = 0;  // of the node tests, the culling tree's box tests (the rest: frustum planes,
-                       // shadow-grid lookups, beam passes, priced as node tests)
+  uint32_t boxes = 0;  // of the node tests, the culling tree's box tests (the rest: frustum planes and
+                       // shadow-grid lookups, priced as node tests)
+  uint32_t beamt = 0;  // reflected-ray beam tests: one per live lane and beam pass (RTX_S_BEAMT)
   __device__ __forceinline__ void test(int k) { tests += (uint32_t)k; }
   __device__ __forceinline__ void node() { ++nodes; }
   __device__ __forceinline__ void box() { ++boxes; }
+  __device__ __forceinline__ void beam() { ++beamt; }
 };
 
 // Shadow any-hit: does test j (root t, validity v) come strictly before the shape's own distance
@@ -1978,10 +1981,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       const double* btab = LDS ? (const double*)lds_tab : p.scene + RTX_HDR_WORDS;
       if (BEAM && sc[RTX_H_TAME] != 0.0 && wave_beam<kBeamStaged && LDS>(btab, nb, ox, oy, oz, dx, dy, dz, bm)) {
         if (st) stat_wave(st, RTX_S_BEAMW);
-        for (int j = 0; j < bm.passes; ++j) {  // a lane's sphere test per pass, priced as two node tests
-          wk.node();                            // (like wave_frustum)
-          wk.node();
-        }
+        for (int j = 0; j < bm.passes; ++j) wk.beam();  // a lane's cone test of one sphere per pass
         nearest_beam(geo, nsph, bm, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
       } else {
         nearest_bvh<false>(sc, ox, oy, oz, dx, dy, dz, tmin, hit, tie, tame, wk);
@@ -2004,6 +2004,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_add(st, RTX_S_TESTS1, wk.tests1);
       stat_add(st, RTX_S_NODES1, wk.nodes1);
       stat_add(st, RTX_S_BOXES, wk.boxes);
+      stat_add(st, RTX_S_BEAMT, wk.beamt);
     }
   }
   const int64_t io = (DEEP && p.mode == 2) || !TREE ? i : pixel_index(lane_id_fresh());

@@ -22,7 +22,7 @@ HDR_WORDS = 64
 GEOM_WORDS = 8
 MAT_WORDS = 24
 MAX_DOMES = 8
-S_WORDS = 265
+S_WORDS = 266
 WS_HDR_BYTES = 256
 FAST_MAX_BOUNCES = 6
 UNBOUNDED_LEVELS = 333
@@ -65,7 +65,7 @@ N_LOX, N_LOY, N_LOZ, N_HIX, N_HIY, N_HIZ, N_FIRST, N_COUNT, N_SKIP, N_MARGIN = r
 (M_G, M_DG, M_TEX, M_TR, M_TG, M_TB, M_A2, M_A2M1, M_1MA2, M_F0, M_1MF0, M_IG, M_TFW, M_TFT, M_HS, M_1MHS,
  M_ROUGH, M_REFL, M_IOR, M_TFIOR) = range(20)
 # stats words
-S_TESTS, S_NODES, S_TESTS1, S_NODES1, S_BEAMW, S_BOXES = 3, 4, 5, 6, 7, 264
+S_TESTS, S_NODES, S_TESTS1, S_NODES1, S_BEAMW, S_BOXES, S_BEAMT = 3, 4, 5, 6, 7, 264, 265
 S_PIXELS, S_DEFERRED, S_TIES, S_RAYS, S_HITS, S_LEVELS, S_WTRACE, S_WSHADE = 0, 1, 2, 8, 72, 64, 136, 200
 
 EXPORTS = (

@@ -651,7 +651,7 @@ class HipRenderer(Renderer):
         return {"pixels": s[L.S_PIXELS], "deferred": s[L.S_DEFERRED], "ties": s[L.S_TIES],
                 "sphere_tests": s[L.S_TESTS], "node_tests": s[L.S_NODES],
                 "sphere_tests_reflected": s[L.S_TESTS1], "node_tests_reflected": s[L.S_NODES1],
-                "beam_searches": s[L.S_BEAMW], "box_tests": s[L.S_BOXES],
+                "beam_searches": s[L.S_BEAMW], "box_tests": s[L.S_BOXES], "beam_tests": s[L.S_BEAMT],
                 "rays": rays[:last], "hits": hits[:last],
                 "waves_traced": s[L.S_WTRACE:L.S_WTRACE + last], "waves_shaded": s[L.S_WSHADE:L.S_WSHADE + last]}
 

@@ -64,6 +64,7 @@ def test_abi_layout_matches_header():
     assert const("RTX_MAT_WORDS") == L.MAT_WORDS
     assert const("RTX_S_WORDS") == L.S_WORDS
     assert const("RTX_S_BOXES") == L.S_BOXES
+    assert const("RTX_S_BEAMT") == L.S_BEAMT
     assert const("RTX_H_CAMOO") == L.H_CAMOO
     assert const("RTX_M_TFIOR") == L.M_TFIOR
     assert const("RTX_G_C0") == L.G_C0
