@@ -107,9 +107,13 @@ def test_c4_8k_64_spheres_full_frame_rows(hip, c4):
 
 
 def test_c4_unbounded_full_frame_rows(hip, c4):
-    """C4 with the reference's unbounded recursion at full size: 467 k chains outlive the fast
-    kernel's 5 levels, so the level-5/11/17 resume records (capacities scaled with the 33 M-pixel
-    frame), both continuation passes and the general kernel all run; sampled rows vs the oracle."""
+    """C4 with the reference's unbounded recursion at full size (the DEEP pipeline: a first pass
+    that defers a chain still alive at level 30 with a 10-word resume record, one continuation pass
+    to level 60, the general kernel beyond; capacities scaled with the 33 M-pixel frame); sampled
+    rows vs the oracle. Whether C4 has chains past level 30 depends on the scene: the records and
+    both resumes are exercised deterministically by test_gpu_parity.py::
+    test_deep_chains_resume_past_levels_30_and_60 (every chain of a trapped-ray scene passes
+    levels 31 and 61), and this test also checks whether any chain of C4 was deferred at all."""
     spec, _, scene, osc = c4
     W, H = 7680, 4320
     r = hip.HipRenderer()  # max_bounces=None
@@ -118,6 +122,14 @@ def test_c4_unbounded_full_frame_rows(hip, c4):
         rows = tiling.tile_rows(H, 8, 64, part)
         want = O.render_rows(osc, rows, None)
         _check(_rows_of(frame, rows, W), want, W, len(rows), f"C4 unbounded part {part}")
+    # the counting render: per-level rays match the capped render's below its cap, and the deepest
+    # level reached is printed (a chain alive at level 30 went through a resume record)
+    rs = hip.HipRenderer(collect_stats=True)
+    rs.render(scene)
+    st = rs.stats()
+    print(f"C4 unbounded: deepest level {len(st['rays']) - 1}, rays past level 30: {sum(st['rays'][31:])}, "
+          f"deferred to the general kernel: {st['deferred']}")
+    assert len(st["rays"]) > 6  # chains beyond the capped kernel's levels exist
 
 
 def test_c5_orbit_32_frame_batch(hip):
