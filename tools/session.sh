@@ -17,7 +17,7 @@
 #   pmc:C            the PMC passes of config C: FETCH_SIZE, WRITE_SIZE, SQ cycles, VALU mix (one pass each)
 #   emul:C           bench.py --emulate-parts 2,4,8 for config C
 #   tiles:C          bench.py --mode tiles --loopback for config C (the RCCL gather path on one GPU)
-#   fuzz:N:SEED      tools/fuzz_parity.py over N random scenes from SEED
+#   fuzz:N:SEED[:SCALE]  tools/fuzz_parity.py over N random scenes from SEED (frames SCALE times larger)
 #   repro:VARIANT[:BYTES]  tools/capture_repro VARIANT (RCCL under graph capture; memcpy|plain|fork|stale)
 #   capture:VARIANT  tools/capture_tiles.py VARIANT (a gathering tiles plan under graph capture)
 #   ab:ARGS          tools/ab.py with ARGS (comma-separated, e.g. ab:--config,C2,--variants,base,x)
@@ -93,8 +93,12 @@ for step in "$@"; do
         --json-out "$O/tiles_$arg.json" ;;
     fuzz)
       n=${arg%%:*}
-      seed=${arg#*:}
-      run "fuzz_$seed" 500 python -u tools/fuzz_parity.py --n "$n" --seed0 "$seed" --out "$O/fuzz_$seed.json" ;;
+      rest=${arg#*:}
+      seed=${rest%%:*}
+      scale=${rest#*:}
+      [ "$scale" = "$rest" ] && scale=1
+      run "fuzz_${seed}_x$scale" 500 python -u tools/fuzz_parity.py --n "$n" --seed0 "$seed" --scale "$scale" \
+        --out "$O/fuzz_${seed}_x$scale.json" ;;
     repro)
       # tools/capture_repro.cpp variant ARG over torch's librccl and HIP runtime (the crash's setting)
       TL=$(python -c "import torch, os; print(os.path.dirname(torch.__file__) + '/lib')")
