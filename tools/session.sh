@@ -76,6 +76,7 @@ for step in "$@"; do
         python3 bench.py $(bargs "$arg") --cpu-seconds 0 --no-secondary ;;
     pmc)
       P="--config $arg --steps 10 --warmup 2 --cpu-seconds 0 --no-secondary --ramp-ms 50"
+      [ "$arg" = C5 ] && P="$P --frames-per-step 32"  # the C5 bench line's launch: 32 frames
       run "pmc_fetch_$arg" 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_$arg/fetch" -o run -- \
         python3 bench.py $P
       run "pmc_write_$arg" 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_$arg/write" -o run -- \
