@@ -111,7 +111,7 @@ for step in "$@"; do
       # tools/capture_tiles.py ARG: a gathering tiles plan captured into a HIP graph (native backtrace on a crash)
       run "capture_$arg" 120 python -u tools/capture_tiles.py "$arg" ;;
     ab)
-      run "ab_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40)" 900 python -u tools/ab.py $(echo "$arg" | tr ',' ' ') ;;
+      run "ab_$(echo "$arg" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-90)" 900 python -u tools/ab.py $(echo "$arg" | tr ',' ' ') ;;
     *)
       echo "unknown step $step"
       exit 2 ;;
