@@ -12,6 +12,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (bench.py with no flags: what the driver runs)
 #   bench2[:C]       bench.py at N = 2 over gloo, both ranks on the one GPU (the N > 1 code path)
+#   unbounded:C      config C's line with the reference's unbounded recursion (HipRenderer's default)
 #   bench:C          bench line of config C (C1 C2 C2main C3 C4 C5), CPU baselines included
 #   rocprof:C        rocprofv3 --kernel-trace --stats of config C's timed bench (no secondary legs)
 #   pmc:C            the PMC passes of config C: FETCH_SIZE, WRITE_SIZE, SQ cycles, VALU mix (one pass each)
@@ -59,6 +60,10 @@ for step in "$@"; do
           --timeout-method thread
       fi ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    unbounded)
+      # the drop-in default: HipRenderer() with the reference's unbounded recursion
+      run "unbounded_$arg" 300 python bench.py $(bargs "$arg") --bounces -1 --cpu-seconds 0 --no-secondary \
+        --json-out "$O/unbounded_$arg.json" ;;
     bench)
       if [ -n "$arg" ]; then
         run "bench_$arg" 300 python bench.py $(bargs "$arg") --cpu-seconds 10 --json-out "$O/bench_$arg.json"
