@@ -231,6 +231,8 @@ class HipRenderer(Renderer):
         # camera launches: the dispatch order learnt per (scene, tile, cap), see _sched_plan
         self.learn_tile_order = bool(learn_tile_order)
         self._sched: dict = {}
+        # uncapped camera renders whose status came back clean (see _check_status)
+        self._clean: dict = {}
         # scenes with image textures: the fast kernel's texturing build (RTX_F_IMAGES) shades them;
         # False defers those pixels to the general kernel (same colours)
         self.fast_textures = bool(fast_textures)
@@ -303,9 +305,21 @@ class HipRenderer(Renderer):
     def _stats_ptr(self):
         return None if self.stats_buffer is None else self.stats_buffer.data_ptr()
 
-    def _check_status(self, ws: torch.Tensor) -> None:
+    def _check_status(self, ws: torch.Tensor, key=None) -> None:
+        """Raise what the kernel flagged in the workspace's status word (renders that can defer chains
+        beyond the fast kernel's levels: a synchronisation). ``key``: a camera launch's identity
+        (scene content, tile, cap; _tile_launch). The kernels are deterministic, so once a render of a
+        key has come back clean an identical render cannot flag anything: later renders of that key
+        skip the read-back and the host round trip (like _general_plan's probe; the status stays in
+        the workspace untouched, clean)."""
         if self.max_bounces is None or self.max_bounces > L.FAST_MAX_BOUNCES:
+            if key is not None and key in self._clean:
+                return
             status = int(ws[:8].view(torch.int32)[1].item())
+            if status == 0 and key is not None:
+                if len(self._clean) >= 64:
+                    self._clean.pop(next(iter(self._clean)))
+                self._clean[key] = True
             if status:
                 ws[4:8].zero_()  # sticky flags: clear for the next call
             if status & L.ST_BAD_SCENE:
@@ -371,7 +385,7 @@ class HipRenderer(Renderer):
                                                   ws.data_ptr(), ws.numel(), self._stats_ptr(), self._stream(), flags,
                                                   _ptr(probe), _ptr(order), _ptr(cost)), "rtx_render_camera")
         self._after_launch(key, probe, cost)
-        self._check_status(ws)
+        self._check_status(ws, key if self.stats_buffer is None else None)  # (the full launch key only)
         return res
 
     def _after_launch(self, key, probe, cost) -> None:
@@ -458,7 +472,7 @@ class HipRenderer(Renderer):
                                            ws.data_ptr(), ws.numel(), flags, _ptr(probe), _ptr(order), _ptr(cost),
                                            _ptr(frame), self._stream()), "rtx_tiles_submit")
         self._after_launch(key, probe, cost)
-        self._check_status(ws)
+        self._check_status(ws, key if self.stats_buffer is None else None)
 
     @_on_device
     def render_batch(self, scenes, out: str | None = None) -> torch.Tensor:

@@ -401,6 +401,35 @@ def test_unbounded_recursion_limit(hip):
         r.render(scene)
 
 
+def test_unbounded_status_read_back_once_per_clean_render(hip, monkeypatch):
+    """An uncapped render reads the kernel's status word back (a host round trip) to raise
+    RecursionError at the call, as the reference does. The kernels are deterministic, so once a
+    render of a (scene content, tile, cap) has come back clean, identical renders skip the read-back;
+    a render that flagged something (trapped rays) is checked, and raises, every time."""
+    r = hip.HipRenderer()  # unbounded, like the reference
+    spec = scenes.readme_spec(64, 36)
+    scene = scenes.build_scene(spec)
+    first = r.render(scene).data.clone()
+    assert len(r._clean) == 1
+    calls = []
+    orig = torch.Tensor.item
+    monkeypatch.setattr(torch.Tensor, "item", lambda self: (calls.append(1), orig(self))[1])
+    again = r.render(scene).data
+    monkeypatch.undo()
+    assert not calls and torch.equal(first, again)
+    assert np.abs(again.cpu().numpy() - O.render(O.scene_from_spec(spec), None)).max() <= ATOL
+    trapped = scenes.readme_spec(8, 8)
+    trapped["spheres"] = [{"center": [0, 0.2, -2], "radius": -5.0,
+                           "shader": {"reflection_gain": 1, "specular_gain": 1.0, "specular_roughness": 0.5,
+                                      "iridescence_gain": 0, "diffuse_gain": 0.5,
+                                      "texture": {"kind": "const", "color": [1, 1, 1]}}}]
+    trapped["lights"][0]["position"] = [0, 0.2, -2]
+    for _ in range(2):
+        with pytest.raises(RecursionError):
+            r.render(scenes.build_scene(trapped))
+    assert len(r._clean) == 1
+
+
 @pytest.mark.parametrize("cap", [61, 80])
 def test_deep_chains_resume_past_levels_30_and_60(hip, cap):
     """every chain deterministically outlives both resume records of the uncapped
