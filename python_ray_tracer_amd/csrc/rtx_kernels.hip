@@ -76,7 +76,8 @@ constexpr int kB5Waves = 4;          // their waves/SIMD
 constexpr int kLvWaves = 5;          // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
 constexpr int kLvWavesSmall = 5;     // ... and of their TREE = false instantiations (scenes below kTreeMinSpheres)
 constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
-constexpr int kDeepWaves = 3;        // waves/SIMD of the DEEP instantiation (records + continuation need registers)
+constexpr int kDeepWaves = 4;        // waves/SIMD of the DEEP instantiation (with the beam at 3 its persistent kernel takes
+                                     // 134 VGPRs; at 4, 128 and 2 spilled: A/B r6ap, unbounded C4 -14%)
 constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
 // Capped kernels (B <= RTX_FAST_MAX_BOUNCES): the bounce chain's colour is accumulated forwards,
 // col = sum_k T_k L_k with T_0 = 1, T_{k+1} = (T_k * 0.5) * g_k and L_k level k's colour with a
@@ -2084,9 +2085,11 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
                               : kForwardFold ? (TP >= 2 ? kFwdWavesPersist : TP ? kFwdWaves : kFwdWavesSmall)
                                              : kFastWavesPerSimd)) void k_render_fast(Params p0) {
   constexpr bool TREE = TP >= 1;
-  // reflected-ray beams (wave_beam): scenes of kPersistMinSpheres and more, capped renders (A/B: C4
-  // -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%)
-  constexpr bool BEAM = TP >= 2 && !DEEP;
+  // reflected-ray beams (wave_beam): the persistent launches, scenes of kPersistMinSpheres and more
+  // (A/B: C4 -5.3%; with 16 spheres the tree walk is cheaper than the beam, C3 +7%, C5 +4%), capped
+  // or not (the DEEP first pass since round 6, with kDeepWaves 4: A/B r6ap, unbounded C4 2,101 ->
+  // 1,800 us)
+  constexpr bool BEAM = TP >= 2;
   extern __shared__ double lds_tab[];
   const Params p = frame_view(p0, blockIdx.z);  // frame of a multi-frame launch (grid z)
   {
