@@ -76,8 +76,10 @@ constexpr int kB5Waves = 4;          // their waves/SIMD
 constexpr int kLvWaves = 5;          // waves/SIMD of the kernels with LDS level slots (96 VGPRs; 5 blocks fit up to 17 spheres)
 constexpr int kLvWavesSmall = 5;     // ... and of their TREE = false instantiations (scenes below kTreeMinSpheres)
 constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
-constexpr int kDeepWaves = 4;        // waves/SIMD of the DEEP instantiation (with the beam at 3 its persistent kernel takes
+constexpr int kDeepWaves = 4;        // waves/SIMD of the persistent DEEP kernel (with the beam at 3 its persistent kernel takes
                                      // 134 VGPRs; at 4, 128 and 2 spilled: A/B r6ap, unbounded C4 -14%)
+constexpr int kDeepWavesTile = 5;    // ... of the one-tile DEEP kernels (TP 1 and 0; A/B r6ar, unbounded: C3 -5.1%,
+                                     // C2 -2.0%, C2main -5.0% against 4, the persistent C4 +-0)
 constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
 // Capped kernels (B <= RTX_FAST_MAX_BOUNCES): the bounce chain's colour is accumulated forwards,
 // col = sum_k T_k L_k with T_0 = 1, T_{k+1} = (T_k * 0.5) * g_k and L_k level k's colour with a
@@ -2080,7 +2082,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2,
           bool IMG = false, int NSPH = 0>
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
-                             (DEEP  ? kDeepWaves
+                             (DEEP  ? (TP >= 2 ? kDeepWaves : kDeepWavesTile)
                               : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
                               : kForwardFold ? (TP >= 2 ? kFwdWavesPersist : TP ? kFwdWaves : kFwdWavesSmall)
                                              : kFastWavesPerSimd)) void k_render_fast(Params p0) {
