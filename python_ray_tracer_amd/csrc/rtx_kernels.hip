@@ -78,7 +78,7 @@ constexpr int kLvWavesSmall = 5;     // ... and of their TREE = false instantiat
 constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
 constexpr int kDeepWaves = 4;        // waves/SIMD of the persistent DEEP kernel (with the beam at 3 its persistent kernel takes
                                      // 134 VGPRs; at 4, 128 and 2 spilled: A/B r6ap, unbounded C4 -14%)
-constexpr int kDeepWavesTile = 5;    // ... of the one-tile DEEP kernels (TP 1 and 0; A/B r6ar, unbounded: C3 -5.1%,
+constexpr int kDeepWavesTile = 5;    // ... of the one-tile first passes (TP 1 and 0; A/B r6ar, unbounded: C3 -5.1%,
                                      // C2 -2.0%, C2main -5.0% against 4, the persistent C4 +-0)
 constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
 // Capped kernels (B <= RTX_FAST_MAX_BOUNCES): the bounce chain's colour is accumulated forwards,
@@ -1683,7 +1683,7 @@ __device__ __forceinline__ void stat_wave(unsigned long long* st, int word) {
 // instead of deferred to the general kernel.
 // NSPH > 0: the scene has exactly NSPH spheres, a compile-time count (the timed small-scene kernels,
 // rtx_small.hip: their sphere loops unroll; A/B r6b, C2 -2.7%); 0: p.nsph at run time.
-template <int B, bool LDS, bool DEEP, bool LVL, bool STATS, bool TREE, bool BEAM, bool IMG = false, int NSPH = 0>
+template <int B, bool LDS, int DEEP, bool LVL, bool STATS, bool TREE, bool BEAM, bool IMG = false, int NSPH = 0>
 __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool first, const double* lds_tab,
                                           bool wave_tile = false) {
   constexpr int FB = fast_block<TREE>();  // threads per block of this instantiation
@@ -1715,13 +1715,13 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
     }
     return (int64_t)bx * FB + wv * 64 + lane;
   };
-  if (p.mode == 0) {
+  if (DEEP != 2 && p.mode == 0) {
     const int lane = threadIdx.x & 63, w = TREE ? wv : (int)(threadIdx.x >> 6);
     col = wave_tile ? bx * WW + (lane % WW) : bx * (WX * WW) + (w % WX) * WW + (lane % WW);
     lr = wave_tile ? by * WH + (lane / WW) : by * (WY * WH) + (w / WX) * WH + (lane / WW);
     active = col < p.width && lr < p.n_rows;
     if constexpr (!TREE) i = (int64_t)lr * p.width + col;  // (kept live: A/B r5v C2 +1.4% recomputed)
-  } else if (!DEEP || p.mode == 1 || p.mode == 3) {
+  } else if (DEEP != 2) {  // (modes 1 and 3)
     i = (int64_t)bx * FB + threadIdx.x;
     active = i < p.n;
   } else {  // continuation: entry `item` of in_list
@@ -1740,7 +1740,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       }
     }
   }
-  const bool cam0 = (p.mode == 0);
+  const bool cam0 = DEEP != 2 && p.mode == 0;
   // per-level counters: the stats instantiation only (the timed kernels compile none of it)
   unsigned long long* const st = STATS ? p.stats : nullptr;
   Work<STATS> wk;
@@ -1815,7 +1815,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   // levels_in_lds, LDS slots indexed by the level (slot j = level kb + j)
   constexpr bool LV = LVL && LDS && B > 0 && !kForwardFold;
   constexpr int NS = B > 0 ? B : 1;
-  constexpr int NL = LV ? level_lds_slots<DEEP>(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
+  constexpr int NL = LV ? level_lds_slots<(DEEP != 0)>(B) : 0;  // levels 0..NL-1 in LDS, NL..B-1 in registers
   constexpr int NR = LV ? (B > NL ? B - NL : 1) : NS;
   double sDli[NR], sDi[NR], sSpec[NR], sVa[NR];
   int sKey[NR];  // hit sphere | checker bit << 16
@@ -1827,7 +1827,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
   // kForwardFold (capped kernels): colour accumulated level by level, thr = T_k
   constexpr bool FWD = kForwardFold;
   double thr = 1.0;
-  if constexpr (FWD && DEEP) {  // a continued chain: its colour so far and the next level's weight
+  if constexpr (FWD && DEEP == 2) {  // a continued chain: its colour so far and the next level's weight
     if (rin) {
       cr = rin[6];
       cg = rin[7];
@@ -1875,7 +1875,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       appended = true;
       rays_through = hits_through = kb + B;
       const int64_t slot =
-          append_deferred(p, deferred_entry(p.mode == 2 || !TREE ? i : pixel_index(lane_id_fresh()), p.frame, kb + B, kb + B));
+          append_deferred(p, deferred_entry(DEEP == 2 || !TREE ? i : pixel_index(lane_id_fresh()), p.frame, kb + B, kb + B));
       if (p.drec && slot >= 0 && slot < p.rec_cap && kb + B == p.drec_level) {
         double* rec = p.drec + slot * rec_words(kb + B);
         double rx = dx, ry = dy, rz = dz;
@@ -1926,7 +1926,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
         deferred = true;
         appended = true;
         rays_through = hits_through = kb + kmax;
-        const int64_t slot = append_deferred(p, deferred_entry(p.mode == 2 || !TREE ? i : pixel_index(lane_id_fresh()),
+        const int64_t slot = append_deferred(p, deferred_entry(DEEP == 2 || !TREE ? i : pixel_index(lane_id_fresh()),
                                                                p.frame, kb + kmax, kb + kmax));
         if (p.drec && slot >= 0 && slot < p.rec_cap) {
           double* rec = p.drec + slot * rec_words(kb + kmax);
@@ -2020,7 +2020,7 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
       stat_add(st, RTX_S_BEAMT, wk.beamt);
     }
   }
-  const int64_t io = (DEEP && p.mode == 2) || !TREE ? i : pixel_index(lane_id_fresh());
+  const int64_t io = DEEP == 2 || !TREE ? i : pixel_index(lane_id_fresh());
   if constexpr (CL) {
     cr = cl[0];
     cg = cl[FB];
@@ -2079,10 +2079,16 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 
 // TP: 0 = no culling tree and no persistent launch (scenes below kTreeMinSpheres), 1 = culling tree,
 // one tile per block (the launch is not persistent), 2 = both (persistent launches)
-template <int B, bool LDS, bool DEEP, bool LVL = levels_in_lds<B, LDS, DEEP>(), bool STATS = false, int TP = 2,
+// DEEP: 0 capped (the chain ends at level B), 1 the first pass of an uncapped render (chains alive at
+// its record level are deferred with a resume record), 2 a continuation pass (mode 2: chains resumed
+// from their records; its own instantiation, so that the first pass compiles no resume code)
+template <int B, bool LDS, int DEEP, bool LVL, bool STATS, int TP, bool IMG, int NSPH>
+__device__ __forceinline__ void k_render_fast_tiles(const Params& p, const double* lds_tab);
+
+template <int B, bool LDS, int DEEP, bool LVL = levels_in_lds<B, LDS, (DEEP != 0)>(), bool STATS = false, int TP = 2,
           bool IMG = false, int NSPH = 0>
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
-                             (DEEP  ? (TP >= 2 ? kDeepWaves : kDeepWavesTile)
+                             (DEEP  ? (TP >= 2 || DEEP == 2 ? kDeepWaves : kDeepWavesTile)
                               : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
                               : kForwardFold ? (TP >= 2 ? kFwdWavesPersist : TP ? kFwdWaves : kFwdWavesSmall)
                                              : kFastWavesPerSimd)) void k_render_fast(Params p0) {
@@ -2113,15 +2119,21 @@ __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
       lds_tab[k] = bw ? beam_word(src[k - RTX_G_IDX + RTX_G_CC], src[k - RTX_G_IDX + RTX_G_RR]) : src[k];
     }
   }
-  if constexpr (DEEP) {
-    if (p.mode == 2) {  // continuation pass: 256 entries of in_list per tile, grid-stride
-      const int64_t count = (int64_t)*p.in_count;
-      for (int64_t t = blockIdx.x; t * fast_block<TREE>() < count; t += gridDim.x) {
-        fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG, NSPH>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
-      }
-      return;
+  if constexpr (DEEP == 2) {  // continuation pass (mode 2): 256 entries of in_list per tile, grid-stride
+    const int64_t count = (int64_t)*p.in_count;
+    for (int64_t t = blockIdx.x; t * fast_block<TREE>() < count; t += gridDim.x) {
+      fast_tile<B, LDS, DEEP, LVL, STATS, TREE, BEAM, IMG, NSPH>(p, (int)t, 0, t == (int64_t)blockIdx.x, lds_tab);
     }
+  } else {
+    k_render_fast_tiles<B, LDS, DEEP, LVL, STATS, TP, IMG, NSPH>(p, lds_tab);
   }
+}
+
+// the camera / explicit-ray launches of k_render_fast (every instantiation but the continuation's)
+template <int B, bool LDS, int DEEP, bool LVL, bool STATS, int TP, bool IMG, int NSPH>
+__device__ __forceinline__ void k_render_fast_tiles(const Params& p, const double* lds_tab) {
+  constexpr bool TREE = TP >= 1;
+  constexpr bool BEAM = TP >= 2;
   if (TP >= 2 && p.n_fetch > 0) {  // (persistent launches are for scenes of kPersistMinSpheres and more)
     // Persistent waves fetching kWaveW x kWaveH tiles, bottom-up (longest work first, as below).
     // Counter c (of n_fetch) hands out tiles c, c + n_fetch, ... . Waves are numbered XCD-major
@@ -2506,7 +2518,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble_rows(const uint8_t* __restr
 // Launches k_render_fast<B, true, deep, lvl, stats, 0>(*params) on s (events e0/e1 as
 // hipExtLaunchKernelGGL's); hipErrorInvalidValue, nothing launched, for an instantiation the unit
 // does not carry.
-__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats, bool img,
+__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, int deep, bool lvl, bool stats, bool img,
                                                                   const void* params, dim3 grid, uint32_t lds,
                                                                   hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 namespace {
@@ -2679,11 +2691,11 @@ dim3 persistent_grid(K kernel, size_t lds, Params& p) {
 // Launches that are not persistent run instantiations without the persistent tile loop (TP 1), and
 // scenes below kTreeMinSpheres, which carry no culling tree (scene_pack.BVH_MIN_SPHERES), ones
 // without the tree walks either (TP 0) (A/B in DESIGN.md §4).
-template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false>
+template <int B, int DEEP, bool LVL, bool STATS, bool IMG = false>
 void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   const bool small = p.nsph < kTreeMinSpheres;  // the TREE = false kernels: fast_block<false>() threads
   const size_t lds = (size_t)p.nsph * kSphWords * sizeof(double) +
-                     (LVL ? (small ? level_lds_bytes<DEEP, false>(B) : level_lds_bytes<DEEP>(B)) : 0) +
+                     (LVL ? (small ? level_lds_bytes<(DEEP != 0), false>(B) : level_lds_bytes<(DEEP != 0)>(B)) : 0) +
                      (kForwardFold && !DEEP && !small && p.n_fetch == 0 ? kColourLdsBytes : 0);  // TP 1
   if (p.n_fetch == 0) {  // one tile per block: the instantiations without the persistent loop
     if (p.nsph < kTreeMinSpheres) {  // TP 0: the rtx_small.hip unit
@@ -2700,7 +2712,7 @@ void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
   hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 2, IMG>), grid, dim3(kFastBlock), (uint32_t)lds, s,
                         prof_event(0), prof_event(1), 0u, p);
 }
-template <int B, bool DEEP, bool LVL>
+template <int B, int DEEP, bool LVL>
 void launch_fast_lds(Params& p, dim3 grid, hipStream_t s) {
   if (p.stats || p.tile_cost) {  // (the cost records of a learning launch live in the STATS kernels)
     launch_fast_lds_s<B, DEEP, LVL, true>(p, grid, s);
@@ -2711,16 +2723,16 @@ void launch_fast_lds(Params& p, dim3 grid, hipStream_t s) {
   }
 }
 
-template <int B, bool DEEP = false>
+template <int B, int DEEP = 0>
 void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
   Params p = p0;
   if (p.nsph <= kLdsMaxSpheres) {
     if constexpr (DEEP) {
       // (forward fold: no level slots, so no LDS for them and the occupancy the registers allow)
       if (!kForwardFold && kLevelsInLds && p.nsph <= kDeepLvMaxSpheres) {
-        launch_fast_lds<B, true, true>(p, grid, s);
+        launch_fast_lds<B, DEEP, true>(p, grid, s);
       } else {
-        launch_fast_lds<B, true, false>(p, grid, s);
+        launch_fast_lds<B, DEEP, false>(p, grid, s);
       }
     } else {
       // caps 3-4 in big scenes: three LDS level slots beside a large scene table leave room for
@@ -2747,7 +2759,9 @@ void launch_fast_b(const Params& p0, dim3 grid, hipStream_t s) {
 }
 
 // caps above kCappedMax or none: kDeepLevels levels, longer chains deferred with a record
-void launch_fast_deep(const Params& p, dim3 grid, hipStream_t s) { launch_fast_b<kDeepLevels, true>(p, grid, s); }
+void launch_fast_deep(const Params& p, dim3 grid, hipStream_t s) { launch_fast_b<kDeepLevels, 1>(p, grid, s); }
+// ... and their continuation passes (mode 2)
+void launch_fast_cont(const Params& p, dim3 grid, hipStream_t s) { launch_fast_b<kDeepLevels, 2>(p, grid, s); }
 
 void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
   switch (B) {
@@ -2851,7 +2865,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
       const int64_t fb = p.nsph < kTreeMinSpheres ? fast_block<false>() : fast_block<true>();
       const int64_t tiles = (n_all + fb - 1) / fb;
       const int64_t cap = 4 * (int64_t)device_cus();
-      launch_fast_deep(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
+      launch_fast_cont(q, dim3((unsigned)(tiles < cap ? tiles : cap)), s);
       if (int e = check_launch("k_render_fast (continuation)")) return e;
       p.in_list = lists[pass];
       p.in_count = counts[pass];

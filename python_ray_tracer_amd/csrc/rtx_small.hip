@@ -8,7 +8,7 @@
 
 namespace {
 
-template <int B, bool DEEP, bool LVL, bool STATS, bool IMG = false, int NSPH = 0>
+template <int B, int DEEP, bool LVL, bool STATS, bool IMG = false, int NSPH = 0>
 hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const Params& p = *static_cast<const Params*>(params);
   hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 0, IMG, NSPH>), grid, dim3(fast_block<false>()), lds,
@@ -20,7 +20,7 @@ hipError_t go(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEve
 // unbounded renders) of each sphere count below kTreeMinSpheres, with the count a compile-time
 // constant (fast_tile's NSPH: the sphere loops unroll; A/B r6b, C2 -2.7%); the counter and
 // texturing kernels keep the run-time count.
-template <int B, bool DEEP, bool LVL>
+template <int B, int DEEP, bool LVL>
 hipError_t go_ns(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   static_assert(kTreeMinSpheres == 8, "one instantiation per sphere count 1..7");
   switch (static_cast<const Params*>(params)->nsph) {
@@ -38,7 +38,7 @@ hipError_t go_ns(const void* params, dim3 grid, uint32_t lds, hipStream_t s, hip
 // the (lvl, stats) instantiations launch_fast_b can request for a scene below kTreeMinSpheres: its
 // table always fits the LDS beside the level slots (levels_in_lds); a DEEP kernel kept every level in
 // LDS (S <= kDeepLvMaxSpheres) before the forward fold
-template <int B, bool DEEP>
+template <int B, int DEEP>
 hipError_t go_b(bool lvl, bool stats, bool img, const void* params, dim3 grid, uint32_t lds, hipStream_t s,
                 hipEvent_t e0, hipEvent_t e1) {
   // (the forward fold keeps no levels: DEEP kernels too run without level slots)
@@ -56,10 +56,14 @@ hipError_t go_b(bool lvl, bool stats, bool img, const void* params, dim3 grid, u
 
 }  // namespace
 
-__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, bool deep, bool lvl, bool stats, bool img,
+__attribute__((visibility("hidden"))) hipError_t rtx_launch_small(int B, int deep, bool lvl, bool stats, bool img,
                                                                   const void* params, dim3 grid, uint32_t lds,
                                                                   hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  if (deep) return B == kDeepLevels ? go_b<kDeepLevels, true>(lvl, stats, img, params, grid, lds, s, e0, e1) : hipErrorInvalidValue;
+  if (deep) {  // 1: an uncapped render's first pass, 2: its continuation passes
+    if (B != kDeepLevels) return hipErrorInvalidValue;
+    return deep == 2 ? go_b<kDeepLevels, 2>(lvl, stats, img, params, grid, lds, s, e0, e1)
+                     : go_b<kDeepLevels, 1>(lvl, stats, img, params, grid, lds, s, e0, e1);
+  }
   switch (B) {
     case 0: return go_b<0, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
     case 1: return go_b<1, false>(lvl, stats, img, params, grid, lds, s, e0, e1);
