@@ -77,7 +77,7 @@ constexpr int kLvWaves = 5;          // waves/SIMD of the kernels with LDS level
 constexpr int kLvWavesSmall = 5;     // ... and of their TREE = false instantiations (scenes below kTreeMinSpheres)
 constexpr int kDeepLvMaxSpheres = 32;  // DEEP kernels with LDS level slots up to this many spheres (3 blocks of 54 KB per CU)
 constexpr int kDeepWaves = 4;        // waves/SIMD of the persistent DEEP kernel (with the beam at 3 its persistent kernel takes
-                                     // 134 VGPRs; at 4, 128 and 2 spilled: A/B r6ap, unbounded C4 -14%)
+                                     // 134 VGPRs; at 4, 128: A/B r6ap, unbounded C4 -14%)
 constexpr int kDeepWavesTile = 5;    // ... of the one-tile first passes (TP 1 and 0; A/B r6ar, unbounded: C3 -5.1%,
                                      // C2 -2.0%, C2main -5.0% against 4, the persistent C4 +-0)
 constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD otherwise: <=128 VGPRs (A/B: faster than 3 waves without spills)
