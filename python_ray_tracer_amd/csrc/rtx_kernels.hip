@@ -95,6 +95,10 @@ constexpr int kFastWavesPerSimd = 4; // __launch_bounds__ min waves per SIMD oth
 constexpr bool kForwardFold = true;
 constexpr int kFwdWavesPersist = 4;  // waves/SIMD of the forward-fold persistent kernels (TP 2; C4: 5 waves 2,025 us)
 constexpr int kFwdWaves = 5;         // ... of the culled one-tile-per-block kernels (TP 1; C3: 4 waves 283.9 us)
+// ... and of their launches of at least kWavesLargeMinPixels pixels (A/B r6aw, 6 waves against 5: C3 (8.3 M
+// pixels) -3.3%, C5's 32-frame launches -3.5%, but one 1080p frame of C5's scene +4%: 80 VGPRs spill)
+constexpr int kFwdWavesLarge = 6;
+constexpr int64_t kWavesLargeMinPixels = int64_t(4) << 20;
 constexpr int kFwdWavesSmall = 5;    // ... and of the TREE = false kernels (TP 0; C2: 6 waves 56.0 us, spills)
 constexpr int kDeepLevels = 5;       // fast-kernel levels before a longer chain is deferred (A/B: 3, 5, 8; the
                                      // 8-level instantiation spills, 3 defers too many pixels)
@@ -2085,10 +2089,12 @@ __device__ __forceinline__ void fast_tile(const Params& p, int bx, int by, bool 
 template <int B, bool LDS, int DEEP, bool LVL, bool STATS, int TP, bool IMG, int NSPH>
 __device__ __forceinline__ void k_render_fast_tiles(const Params& p, const double* lds_tab);
 
+// WAVES > 0: that many waves/SIMD instead of the rule below (kFwdWavesLarge)
 template <int B, bool LDS, int DEEP, bool LVL = levels_in_lds<B, LDS, (DEEP != 0)>(), bool STATS = false, int TP = 2,
-          bool IMG = false, int NSPH = 0>
+          bool IMG = false, int NSPH = 0, int WAVES = 0>
 __global__ __launch_bounds__(fast_block<(TP >= 1)>(),
-                             (DEEP  ? (TP >= 2 || DEEP == 2 ? kDeepWaves : kDeepWavesTile)
+                             WAVES > 0 ? WAVES
+                             : (DEEP  ? (TP >= 2 || DEEP == 2 ? kDeepWaves : kDeepWavesTile)
                               : LVL ? (B >= 5 ? kB5Waves : TP ? kLvWaves : kLvWavesSmall)
                               : kForwardFold ? (TP >= 2 ? kFwdWavesPersist : TP ? kFwdWaves : kFwdWavesSmall)
                                              : kFastWavesPerSimd)) void k_render_fast(Params p0) {
@@ -2703,6 +2709,13 @@ void launch_fast_lds_s(Params& p, dim3 grid, hipStream_t s) {
           rtx_launch_small(B, DEEP, LVL, STATS, IMG, &p, grid, (uint32_t)lds, s, prof_event(0), prof_event(1));
       if (e != hipSuccess) g_small_err = e;
     } else {
+      if constexpr (!DEEP && !STATS && !IMG && kForwardFold) {
+        if ((int64_t)p.n * p.n_frames >= kWavesLargeMinPixels) {  // a large launch: more waves (kFwdWavesLarge)
+          hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 1, IMG, 0, kFwdWavesLarge>), grid,
+                                dim3(kFastBlock), (uint32_t)lds, s, prof_event(0), prof_event(1), 0u, p);
+          return;
+        }
+      }
       hipExtLaunchKernelGGL((k_render_fast<B, true, DEEP, LVL, STATS, 1, IMG>), grid, dim3(kFastBlock), (uint32_t)lds,
                             s, prof_event(0), prof_event(1), 0u, p);
     }

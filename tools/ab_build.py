@@ -38,7 +38,8 @@ def trim(src: str, caps: set) -> str:
             sub(f"    case {b}: launch_fast_b<{b}>(p, grid, s); break;\n", "")
     if 6 not in caps:
         sub("    default: launch_fast_b<6>(p, grid, s); break;", "    default: break;")
-    sub("{ launch_fast_b<kDeepLevels, true>(p, grid, s); }", "{}")
+    sub("{ launch_fast_b<kDeepLevels, 1>(p, grid, s); }", "{}")
+    sub("{ launch_fast_b<kDeepLevels, 2>(p, grid, s); }", "{}")
     sub("    launch_fast_lds_s<B, DEEP, LVL, true>(p, grid, s);", "    launch_fast_lds_s<B, DEEP, LVL, false>(p, grid, s);")
     return src
 
