@@ -60,15 +60,25 @@ def test_c1_readme_960x540_full_frame(hip):
 
 
 def test_c3_4k_16_spheres_full_frame(hip):
-    """configs[2]: 3840x2160, 16 spheres + ground, B=4, the whole frame against the oracle."""
+    """configs[2]: 3840x2160, 16 spheres + ground, B=4, the whole frame against the oracle. The
+    whole frame's launch (8.3 M pixels) runs the one-tile kernel built for 6 waves/SIMD
+    (kFwdWavesLarge, launches of 4 M pixels and more); three interleaved row tiles of 2.8 M pixels
+    each run the 5-wave build, and give the same rows bit for bit."""
     spec, B = scenes.CONFIGS["C3"]()
     r = hip.HipRenderer(max_bounces=B, collect_stats=True)
-    got = r.render(scenes.build_scene(spec)).data.cpu().numpy()
+    scene = scenes.build_scene(spec)
+    frame = r.render(scene).data
+    got = frame.cpu().numpy()
     st = O.TraceStats()
     want = O.render(O.scene_from_spec(spec), B, stats=st)
     _check(got, want, 3840, 2160, "C3")
     s = r.stats()
     assert s["rays"] == st.rays and s["hits"] == st.hits
+    r5 = hip.HipRenderer(max_bounces=B)
+    for part in range(3):
+        rows = tiling.tile_rows(2160, 8, 3, part)
+        assert 3840 * len(rows) < 4 << 20
+        assert np.array_equal(r5.render_tile(scene, 8, 3, part).cpu().numpy(), _rows_of(frame, rows, 3840)), part
 
 
 # row tiles of the 64-way interleaved split of C4 (8-row blocks) checked against the oracle
