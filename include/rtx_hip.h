@@ -255,12 +255,11 @@ int rtx_render_camera(const double* scene, int n_spheres, int width, int height,
  *    that receives, in stream order, the number of rays the fast kernel deferred in this launch
  *    (ties, longer chains); written by the general kernel, so it is left untouched when that kernel
  *    is skipped;
- *  - flags RTX_F_NO_GENERAL: for a capped render (0 <= max_bounces <= RTX_FAST_MAX_BOUNCES) whose
- *    identical earlier launch (same blob content, tile, cap) deferred no ray, the general kernel is
- *    not launched (the render is deterministic, so it defers none again). Passing it for a render
- *    that does defer rays leaves those pixels unwritten and raises the sticky RTX_ST_UNRENDERED
- *    flag (the workspace counters stay clean, so later calls are unaffected). Uncapped renders
- *    ignore it. */
+ *  - flags RTX_F_NO_GENERAL: for a render whose identical earlier launch (same blob content, tile,
+ *    cap) deferred no ray, the general kernel is not launched — nor, for an uncapped render, the
+ *    continuation pass — (the render is deterministic, so it defers none again). Passing it for a
+ *    render that does defer rays leaves those pixels unwritten and raises the sticky
+ *    RTX_ST_UNRENDERED flag (the workspace counters stay clean, so later calls are unaffected). */
 #define RTX_F_NO_GENERAL 1u
 /* RTX_F_IMAGES: the scene has image-textured spheres (RTX_TEX_IMAGE). A capped render then runs the
  * fast kernel's texturing build, which shades those hits itself (the texel lookup compiled in);

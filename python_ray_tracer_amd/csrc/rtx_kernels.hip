@@ -2789,7 +2789,8 @@ void launch_fast(int B, const Params& p, dim3 grid, hipStream_t s) {
 }
 static_assert(RTX_FAST_MAX_BOUNCES == 6, "launch_fast switch covers 0..6");
 
-// no_general: the caller knows this exact (capped) render defers no ray (rtx_render_camera_ex)
+// no_general: the caller knows this exact render defers no ray (rtx_render_camera_ex): no general
+// kernel, and for an uncapped render no continuation pass either
 int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s, bool no_general = false) {
   if (p.nsph <= 0 || p.nsph > RTX_MAX_SPHERES) return fail(RTX_E_ARG, "n_spheres out of range%s (%lld)", "", p.nsph);
   if (!p.scene || !workspace) return fail(RTX_E_ARG, "null pointer argument%s", "");
@@ -2817,7 +2818,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   // The fast kernel renders every ray up to min(cap, RTX_FAST_MAX_BOUNCES) levels; a pixel whose
   // chain outlives that (a larger or no cap) is deferred, like a tie, to the general kernel.
   const bool capped = p.max_bounces >= 0 && p.max_bounces <= kCappedMax;
-  p.no_general = no_general && capped ? 1 : 0;
+  p.no_general = no_general ? 1 : 0;
   p.n_workers = workers_for(n_all, p.max_bounces);
   p.stack_levels = stack_levels_for(p.max_bounces);
   {
@@ -2854,7 +2855,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
   p.in_count = hdr + RTX_WS_COUNT;
   p.in_rec = capped ? nullptr : rec1;
   p.in_level = kForwardFold ? kFirstPassLevels : kDeepLevels;
-  if (!capped && p.n_frames == 1) {
+  if (!capped && p.n_frames == 1 && !no_general) {
     // continuation passes: chains deferred for depth go on for kDeepLevels + 1 more levels in
     // the register-resident kernel, twice; ties and what is still alive after them go to the
     // general kernel
@@ -2888,7 +2889,7 @@ int run_render(Params& p, void* workspace, size_t workspace_bytes, hipStream_t s
     }
   }
   // deferred rays: ties, and chains longer than the fast kernel's levels
-  if (no_general && capped) return RTX_OK;
+  if (no_general) return RTX_OK;  // (an uncapped render: nor the continuation pass)
   hipLaunchKernelGGL(k_render_general, dim3((unsigned)(p.n_workers / 64)), dim3(64), 0, s, p);
   return check_launch("k_render_general");
 }

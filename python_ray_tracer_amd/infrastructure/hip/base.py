@@ -226,7 +226,7 @@ class HipRenderer(Renderer):
         self.color_dtype = color_dtype
         self.device = _resolve_device(device)
         self._scene_cache: dict = {}
-        # capped camera renders known to defer no ray (or probing): see _general_plan
+        # camera renders known to defer no ray (or probing): see _general_plan
         self._defers: dict = {}
         # camera launches: the dispatch order learnt per (scene, tile, cap), see _sched_plan
         self.learn_tile_order = bool(learn_tile_order)
@@ -271,8 +271,9 @@ class HipRenderer(Renderer):
         return self._ws
 
     def _general_plan(self, key):
-        """(flags, probe) for a capped camera render identified by ``key`` (scene content, tile,
-        cap). The tie/deep kernel (k_render_general) runs after every fast launch; when a frame
+        """(flags, probe) for a camera render identified by ``key`` (scene content, tile, cap).
+        The tie/deep kernel (k_render_general) runs after every fast launch (and, uncapped, the
+        continuation pass before it); when a frame
         defers no ray it only reads three zero counters, but it is still a launch (about 2.4% of a
         1080p C2 frame). The first render of a key probes: the library writes the launch's
         deferred count into a device word, copied to pinned memory behind an event. Once that
@@ -411,12 +412,12 @@ class HipRenderer(Renderer):
         flags, probe, order, cost = 0, None, None, None
         if key is not None and self.fast_textures and any(sp[2][0] == L.TEX_IMAGE for sp in key[0][0]):
             flags = L.F_IMAGES  # image-textured spheres shaded by the fast kernel, not deferred
-        capped = self.max_bounces is not None and self.max_bounces <= L.FAST_MAX_BOUNCES
         if key is not None and self.stats_buffer is None:
             key = (key, row_block, n_parts, part, part_run, self.max_bounces)
-            if capped:
-                gflags, probe = self._general_plan(key)
-                flags |= gflags
+            # capped and uncapped alike (an uncapped render that defers nothing also skips the
+            # continuation pass: unbounded C2 -4 us per frame)
+            gflags, probe = self._general_plan(key)
+            flags |= gflags
             if self.learn_tile_order:
                 order, cost = self._sched_plan(key, int(scene.camera.width), rows, n_spheres)
         if torch.cuda.is_current_stream_capturing():

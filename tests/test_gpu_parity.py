@@ -137,6 +137,30 @@ def test_general_launch_skipped_only_when_nothing_is_deferred(hip, golden_meta, 
     assert len(r._defers) == 3
 
 
+def test_uncapped_skips_continuation_and_general_only_when_nothing_is_deferred(hip):
+    """The probe also serves uncapped renders (round 6): once the first render of a key has deferred
+    nothing, later renders skip the continuation pass and the general kernel (RTX_F_NO_GENERAL); a
+    scene whose chains all outlive the first pass's level-30 record keeps them. Every render of both
+    equals the oracle's, three times over (the later ones with the flag decided)."""
+    spec = scenes.random_spec(16, 3, 64, 36)  # no chain reaches level 30
+    trap = scenes.readme_spec(12, 8)  # every chain passes level 30 (test_deep_chains_resume_...)
+    trap["spheres"] = [{"center": [0, 0.2, -2], "radius": -5.0,
+                        "shader": {"reflection_gain": 1, "specular_gain": 1.0, "specular_roughness": 0.5,
+                                   "iridescence_gain": 0.05, "diffuse_gain": 0.5,
+                                   "texture": {"kind": "const", "color": [0.9, 0.7, 0.4]}}}]
+    trap["lights"][0]["position"] = [0, 0.2, -2]
+    for sp, cap, skips in ((spec, None, True), (trap, 40, False)):
+        want = O.render(O.scene_from_spec(sp), cap)
+        r = hip.HipRenderer(max_bounces=cap, color_dtype=torch.float64)
+        assert r.max_bounces is None or r.max_bounces > hip._lib.FAST_MAX_BOUNCES  # the uncapped pipeline
+        scene = scenes.build_scene(sp)
+        for _ in range(3):
+            got = r.render_tile(scene).cpu().numpy()  # .cpu() synchronises: the probe has landed
+            assert np.abs(got - want).max() <= ATOL, (cap, np.abs(got - want).max())
+        (state,) = r._defers.values()
+        assert state is skips, cap
+
+
 def test_camera_ex_flags_are_checked(hip):
     from python_ray_tracer_amd.infrastructure.hip import _lib as L
 
