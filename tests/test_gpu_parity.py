@@ -161,6 +161,34 @@ def test_uncapped_skips_continuation_and_general_only_when_nothing_is_deferred(h
         assert state is skips, cap
 
 
+@pytest.mark.parametrize("cap", [3, None])
+def test_scene_above_the_lds_table(hip, cap):
+    """Scenes of more spheres than the LDS table holds (kLdsMaxSpheres = 128) run the builds that read
+    the sphere table from global memory. test_large_scene_without_lds_table renders through the
+    counting (STATS) builds; this one through the counter-free builds a plain render runs: the
+    persistent launch (camera frame) and, uncapped, its first pass, continuation pass and general
+    kernel, then the explicit-ray mode (HipCameraRays materialised). 150 spheres against the oracle;
+    the counters of a counting render too."""
+    spec = scenes.random_spec(150, 7, 56, 32)
+    osc = O.scene_from_spec(spec)
+    st = O.TraceStats()
+    want = O.render(osc, cap, stats=st)
+    r = hip.HipRenderer(max_bounces=cap, color_dtype=torch.float64)
+    scene = scenes.build_scene(spec)
+    for _ in range(2):  # (the second render with the deferral probe landed)
+        got = r.render_tile(scene).cpu().numpy()
+        assert np.abs(got - want).max() <= ATOL, (cap, np.abs(got - want).max())
+    dirs = r.get_ray_directions(scene.camera)
+    assert dirs.data.shape[-1] == 56 * 32 or dirs.data.numel() == 3 * 56 * 32  # materialised: the explicit-ray mode
+    rays = r.raytrace_scene(scene.camera.position, dirs, scene).data.cpu().numpy()
+    assert np.abs(rays - want).max() <= ATOL
+    rs = hip.HipRenderer(max_bounces=cap, collect_stats=True)
+    rs.render(scene)
+    s = rs.stats()
+    n = min(len(st.rays), hip._lib.S_LEVELS)
+    assert s["rays"][:n] == st.rays[:n] and s["hits"][:n] == st.hits[:n]
+
+
 def test_camera_ex_flags_are_checked(hip):
     from python_ray_tracer_amd.infrastructure.hip import _lib as L
 
