@@ -4,7 +4,7 @@
     python tools/resource_usage.py [SOURCE.hip ...]      (default: csrc/rtx_kernels.hip)
 
 Compiles each source for gfx950 with the library's flags (device only, in parallel) and prints one
-row per instantiation: template arguments <B, LDS, DEEP, LVL, STATS, TP>, VGPRs, VGPR spills, scratch
+row per instantiation: template arguments <B, LDS, DEEP, LVL, STATS, TP, IMG, NSPH[, WAVES]>, VGPRs, VGPR spills, scratch
 bytes per lane and occupancy, side by side for the sources given (A/B variants of the kernel file
 must sit next to it, e.g. csrc/_ab_x.hip, so that its relative #include resolves).
 """
@@ -25,8 +25,12 @@ FLAGS = [f for f in _build.HIPCC_FLAGS if f not in ("-fPIC", "-shared")]
 
 
 def demangle_args(name: str) -> str:
-    m = re.search(r"k_render_fastILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)E", name)
-    return "<{},{},{},{},{},{},{}>".format(*m.groups()) if m else name
+    # <B, LDS, DEEP (bool before round 6's split, int 0/1/2 since), LVL, STATS, TP, IMG[, NSPH[, WAVES]]>
+    m = re.search(r"k_render_fastILi(\d+)ELb(\d)EL[bi](\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)E(?:Li(\d+)E)?(?:Li(\d+)E)?", name)
+    if not m:
+        return name
+    g = [x for x in m.groups() if x is not None]
+    return "<" + ",".join(g) + ">"
 
 
 def usage(text: str) -> dict:
